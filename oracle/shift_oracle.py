@@ -1,0 +1,218 @@
+"""CPU oracle for the learnable fractional temporal shift (TEST INFRASTRUCTURE ONLY).
+
+This module is the parity checker for the HIP temporal-shift kernels. Only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import it, and only as the checker: the product path never routes through it.
+
+It restates, term by term and in float32 with one rounding per operation (no
+fused multiply-add), the reference CUDA extension
+``model/Temporal_shift/cuda/shift_cuda_kernel.cu``:
+
+* :func:`shift_forward`          <- ``shift_cuda_forward_kernel``      (.cu:11-76) + launcher (.cu:405-431)
+* :func:`shift_bottom_backward`  <- ``Shift_Bottom_Backward_Stride1`` (.cu:78-152) and
+                                   ``Shift_Bottom_Backward`` (stride 2, .cu:155-256)
+* :func:`shift_position_backward`<- ``Shift_Position_Backward``       (.cu:277-363)
+* :func:`reduce_position_grad`   <- ATen ``mean(0)``/``sum(2)``/``sum(1)`` (.cu:501-509)
+* :func:`apply_shift_constraint` <- ``applyShiftConstraint``          (.cu:370-395)
+* :func:`shift_backward`         <- ``shift_cuda_backward``           (.cu:433-523)
+
+and the Python glue ``model/Temporal_shift/cuda/shift.py:9-30`` (``ypos + 0.5`` for
+stride != 1, computed in float32, is applied by the caller exactly as there).
+
+Index arithmetic (``floorf`` → int, bounds tests, C++ remainder/quotient for the
+stride-2 bottom backward) is reproduced bit-exactly.
+
+Parity pinning: the reference's CUDA extension cannot be built or run in this image
+(nvcc absent; its binding does not compile against torch 2.10; the prebuilt .so is
+CUDA 9 / sm_30 and is never loaded). This restatement is pinned by (a) a second,
+independent scalar-loop restatement in :mod:`oracle.shift_loops` checked element by
+element, (b) hand-derived known-answer vectors (integer shifts are exact
+translations; the reference ``demo.py`` case), and (c) the exact-adjoint property of
+the bottom backward, all in ``tests/test_oracle_shift.py``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+F32 = np.float32
+ONE = F32(1.0)
+
+
+def _floor_int(v: np.ndarray) -> np.ndarray:
+    """``int x1 = floorf(x)`` (.cu:49) on a float32 vector."""
+    return np.floor(v.astype(F32)).astype(np.int64)
+
+
+def _taps(plane: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.ndarray:
+    """Gather ``plane[..., hh, ww]`` with zero outside [0,H)x[0,W) (.cu:56-68).
+
+    plane: (B, C, H, W); hh: (C, Ho, 1) int; ww: (C, 1, Wo) int -> (B, C, Ho, Wo).
+    """
+    B, C, H, W = plane.shape
+    hh_b, ww_b = np.broadcast_arrays(hh, ww)
+    valid = (hh_b >= 0) & (ww_b >= 0) & (hh_b < H) & (ww_b < W)
+    hc = np.clip(hh_b, 0, H - 1)
+    wc = np.clip(ww_b, 0, W - 1)
+    cidx = np.arange(C)[:, None, None]
+    out = plane[:, cidx, hc, wc]
+    return np.where(valid[None], out, F32(0)).astype(F32)
+
+
+def _bilinear(q11, q21, q12, q22, dx, dy):
+    """``q11*(1-dx)*(1-dy) + q21*dx*(1-dy) + q12*(1-dx)*dy + q22*dx*dy`` (.cu:73),
+    evaluated left to right in float32 (each product/sum rounded once)."""
+    omdx = ONE - dx
+    omdy = ONE - dy
+    t1 = (q11 * omdx) * omdy
+    t2 = (q21 * dx) * omdy
+    t3 = (q12 * omdx) * dy
+    t4 = (q22 * dx) * dy
+    return (((t1 + t2) + t3) + t4).astype(F32)
+
+
+def _frac(pos: np.ndarray):
+    """Per-channel integer/fractional split: ``x1=floorf(x); dx=x-x1`` (.cu:49-71)."""
+    pos = pos.astype(F32)
+    i1 = _floor_int(pos)
+    d = (pos - i1.astype(F32)).astype(F32)
+    return i1, d
+
+
+def shift_forward(inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray, stride: int) -> np.ndarray:
+    """Forward temporal shift. ``ypos`` must already carry the +0.5 for stride != 1
+    (``shift.py:17-18``). Output shape (B, C, H // stride, W) (.cu:408)."""
+    inp = np.ascontiguousarray(inp, dtype=F32)
+    B, C, H, W = inp.shape
+    Ho = H // stride
+    x1, dx = _frac(xpos)
+    y1, dy = _frac(ypos)
+    h = np.arange(Ho)[None, :, None] * stride                # h_offset = h*stride
+    w = np.arange(W)[None, None, :]                          # w_offset = w
+    hy1 = h + y1[:, None, None]
+    hy2 = hy1 + 1
+    wx1 = w + x1[:, None, None]
+    wx2 = wx1 + 1
+    q11 = _taps(inp, hy1, wx1)
+    q21 = _taps(inp, hy1, wx2)
+    q12 = _taps(inp, hy2, wx1)
+    q22 = _taps(inp, hy2, wx2)
+    dxb = dx[None, :, None, None]
+    dyb = dy[None, :, None, None]
+    return _bilinear(q11, q21, q12, q22, dxb, dyb)
+
+
+def _taps_stride2_top(gout: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.ndarray:
+    """Stride-2 bottom-backward tap (.cu:203-248): a tap is taken only when
+    ``h_im % 2 == 0`` (C++ remainder: truncated toward zero), then ``h_im/2``
+    (C++ quotient, truncated) is bounds-checked against the top grid."""
+    B, C, Ht, Wt = gout.shape
+    hh_b, ww_b = np.broadcast_arrays(hh, ww)
+    even = np.fmod(hh_b, 2) == 0
+    hq = np.trunc(hh_b / 2).astype(np.int64)
+    valid = even & (hq >= 0) & (ww_b >= 0) & (hq < Ht) & (ww_b < Wt)
+    hc = np.clip(hq, 0, Ht - 1)
+    wc = np.clip(ww_b, 0, Wt - 1)
+    cidx = np.arange(C)[:, None, None]
+    out = gout[:, cidx, hc, wc]
+    return np.where(valid[None], out, F32(0)).astype(F32)
+
+
+def shift_bottom_backward(gout: np.ndarray, xpos: np.ndarray, ypos: np.ndarray,
+                          H: int, stride: int) -> np.ndarray:
+    """Input gradient: bilinear sample of ``grad_output`` at the reversed position
+    ``(-xpos, -ypos)`` over the bottom grid (.cu:78-152 stride 1, .cu:155-256 stride 2)."""
+    gout = np.ascontiguousarray(gout, dtype=F32)
+    B, C, Ht, W = gout.shape
+    x1, dx = _frac(-xpos.astype(F32))
+    y1, dy = _frac(-ypos.astype(F32))
+    h = np.arange(H)[None, :, None]
+    w = np.arange(W)[None, None, :]
+    hy1 = h + y1[:, None, None]
+    hy2 = hy1 + 1
+    wx1 = w + x1[:, None, None]
+    wx2 = wx1 + 1
+    if stride == 1:
+        tap = _taps
+    elif stride == 2:
+        tap = _taps_stride2_top
+    else:  # the reference hard-codes stride 2 in its non-unit branch (.cu:172-174)
+        raise ValueError("reference backward supports stride 1 and 2 only")
+    q11 = tap(gout, hy1, wx1)
+    q21 = tap(gout, hy1, wx2)
+    q12 = tap(gout, hy2, wx1)
+    q22 = tap(gout, hy2, wx2)
+    return _bilinear(q11, q21, q12, q22, dx[None, :, None, None], dy[None, :, None, None])
+
+
+def shift_position_backward(inp: np.ndarray, gout: np.ndarray, xpos: np.ndarray,
+                            ypos: np.ndarray, stride: int):
+    """Per-output-element position gradients ``val_x*g`` and ``val_y*g`` (.cu:277-363).
+
+    Returns the two (B, C, Ho, W) temporaries the reference materialises (.cu:480-481)."""
+    inp = np.ascontiguousarray(inp, dtype=F32)
+    gout = np.ascontiguousarray(gout, dtype=F32)
+    B, C, H, W = inp.shape
+    Ho = H // stride
+    ix1, dx = _frac(xpos)
+    iy1, dy = _frac(ypos)
+    h = np.arange(Ho)[None, :, None] * stride
+    w = np.arange(W)[None, None, :]
+    h1 = h + iy1[:, None, None]
+    h2 = h1 + 1
+    w1 = w + ix1[:, None, None]
+    w2 = w1 + 1
+    q11 = _taps(inp, h1, w1)
+    q21 = _taps(inp, h1, w2)
+    q12 = _taps(inp, h2, w1)
+    q22 = _taps(inp, h2, w2)
+    dxb = dx[None, :, None, None]
+    dyb = dy[None, :, None, None]
+    # val_x = (1-dy)*(q21-q11)+dy*(q22-q12); val_y = (1-dx)*(q12-q11)+dx*(q22-q21)  (.cu:343-344)
+    val_x = ((ONE - dyb) * (q21 - q11) + dyb * (q22 - q12)).astype(F32)
+    val_y = ((ONE - dxb) * (q12 - q11) + dxb * (q22 - q21)).astype(F32)
+    return (val_x * gout).astype(F32), (val_y * gout).astype(F32)
+
+
+def reduce_position_grad(g_bchw: np.ndarray) -> np.ndarray:
+    """``mean`` over batch, then ``sum`` over W, then ``sum`` over H (.cu:501-509).
+
+    The reference's reduction order inside each ATen op is an implementation detail of
+    ATen/CUDA; only the sign (and zero-ness) of the result is observable after
+    :func:`apply_shift_constraint`. float64 accumulation keeps the sign robust."""
+    g = g_bchw.astype(np.float64)
+    return g.mean(axis=0).sum(axis=2).sum(axis=1).astype(F32)
+
+
+def apply_shift_constraint(gx: np.ndarray, gy: np.ndarray):
+    """``applyShiftConstraint`` (.cu:370-395), including its float/double promotions:
+    ``dr = sqrt(dy*dy)`` in float; ``dx/dr*0.0`` and ``dy/dr*0.01`` are float
+    quotients times *double* literals, rounded to float on store; the ``dr == 0``
+    branch stores ``0.0`` and ``0.0001`` (as float)."""
+    gx = gx.astype(F32)
+    gy = gy.astype(F32)
+    dr = np.sqrt((gy * gy).astype(F32)).astype(F32)
+    nz = dr != 0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        qx = (gx / np.where(nz, dr, ONE)).astype(F32)
+        qy = (gy / np.where(nz, dr, ONE)).astype(F32)
+    out_x = np.where(nz, (qx.astype(np.float64) * 0.0).astype(F32), F32(0.0))
+    out_y = np.where(nz, (qy.astype(np.float64) * 0.01).astype(F32), F32(0.0001))
+    return out_x.astype(F32), out_y.astype(F32)
+
+
+def shift_backward(gout: np.ndarray, inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray,
+                   stride: int):
+    """``shift_cuda_backward`` (.cu:433-523): returns ``(grad_input, grad_xpos, grad_ypos)``.
+    ``ypos`` is the (possibly +0.5-shifted) value saved by the forward (``shift.py:21``)."""
+    H = inp.shape[2]
+    gin = shift_bottom_backward(gout, xpos, ypos, H, stride)
+    gxb, gyb = shift_position_backward(inp, gout, xpos, ypos, stride)
+    gx, gy = apply_shift_constraint(reduce_position_grad(gxb), reduce_position_grad(gyb))
+    return gin, gx, gy
+
+
+def effective_ypos(ypos: np.ndarray, stride: int) -> np.ndarray:
+    """``ShiftFunction.forward``'s ``ypos = ypos + 0.5`` for stride != 1 (``shift.py:14-18``),
+    a float32 add."""
+    ypos = ypos.astype(F32)
+    return ypos if stride == 1 else (ypos + F32(0.5)).astype(F32)
