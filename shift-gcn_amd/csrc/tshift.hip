@@ -1,0 +1,372 @@
+// Learnable fractional temporal shift on gfx950 (MI355X).
+//
+// Replaces the reference CUDA extension `shift_cuda`
+// (model/Temporal_shift/cuda/shift_cuda_kernel.cu, shift_cuda.cpp:44-47):
+//   forward : shift_cuda_forward_kernel (.cu:11-76) + launcher (.cu:405-431)
+//   backward: Shift_Bottom_Backward_Stride1 / Shift_Bottom_Backward (.cu:78-256),
+//             Shift_Position_Backward (.cu:277-363), the ATen mean/sum reductions
+//             (.cu:501-509) and applyShiftConstraint (.cu:370-395).
+//
+// MI355X design (not a translation):
+//  * one 256-thread workgroup per (n·m, c) plane of the (N·M, C, T, V) layout: the
+//    plane is one contiguous T·V run, so the shift's integer part is an address offset
+//    and all four taps of a wave are coalesced (they re-hit the same lines in L1);
+//  * per-channel shift geometry is computed once per workgroup (SGPR-uniform);
+//  * the backward fuses the input gradient, the position-gradient products and their
+//    per-plane reduction in ONE pass: the reference's two (B,C,Ho,W) temporaries
+//    (.cu:480-481, 2x245.8 MB at NTU l2) and its three ATen reductions never exist;
+//    per-plane partials are combined in a fixed order by a C-thread finalize kernel,
+//    so gx/gy are bit-reproducible run to run;
+//  * optional fusions used by the Shift_tcn pipeline: a per-channel affine applied to
+//    every in-range input tap (BatchNorm apply folded into the shift's gather), ReLU
+//    masking of the input gradient, and per-plane output moments (BatchNorm stats of
+//    the shift output, two-pass exact within a plane, Chan-merged in double later).
+//
+// Arithmetic follows the reference expression order with contraction disabled, so
+// outputs are bit-identical to the oracle restatement (oracle/shift_oracle.py).
+#include "common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace sgcn {
+namespace {
+
+constexpr int kThreads = 256;
+
+struct Geom {
+  int x1, y1;
+  float dx, dy;
+};
+
+// `int x1 = floorf(x); dx = x - x1;` (.cu:49-71)
+__device__ __forceinline__ Geom make_geom(float x, float y) {
+  Geom g;
+  g.x1 = (int)floorf(x);
+  g.y1 = (int)floorf(y);
+  g.dx = x - (float)g.x1;
+  g.dy = y - (float)g.y1;
+  return g;
+}
+
+// q11*(1-dx)*(1-dy) + q21*dx*(1-dy) + q12*(1-dx)*dy + q22*dx*dy, left to right (.cu:73)
+__device__ __forceinline__ float blend(float q11, float q21, float q12, float q22, float dx,
+                                       float dy) {
+  const float omdx = 1.f - dx, omdy = 1.f - dy;
+  return q11 * omdx * omdy + q21 * dx * omdy + q12 * omdx * dy + q22 * dx * dy;
+}
+
+// Position of element `o` of a W-wide plane, advanced by blockDim per step without
+// integer division in the loop.
+struct Walker {
+  int h, w, dh, dw, W;
+  __device__ __forceinline__ Walker(int o0, int step, int W_) : W(W_) {
+    h = o0 / W_;
+    w = o0 - h * W_;
+    dh = step / W_;
+    dw = step - dh * W_;
+  }
+  __device__ __forceinline__ void next() {
+    h += dh;
+    w += dw;
+    if (w >= W) { w -= W; ++h; }
+  }
+};
+
+template <bool AFFINE>
+__device__ __forceinline__ float tap(const float* __restrict__ p, bool ok, float a, float b) {
+  if (!ok) return 0.f;
+  const float v = *p;
+  return AFFINE ? v * a + b : v;
+}
+
+// ------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------
+template <int EPT, bool AFFINE, bool STATS>
+__global__ __launch_bounds__(kThreads) void tshift_fwd_kernel(
+    const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
+    const float* __restrict__ ypos, const float* __restrict__ scale,
+    const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
+    int Ho, int stride) {
+  __shared__ float red[2 * kThreads / 64];
+  const int plane = blockIdx.x;
+  const int c = plane % C;
+  const float* __restrict__ src = in + (size_t)plane * Hb * W;
+  float* __restrict__ dst = out + (size_t)plane * Ho * W;
+  const float y = stride == 1 ? ypos[c] : ypos[c] + 0.5f;   // shift.py:17-18 (fp32 add)
+  const Geom g = make_geom(xpos[c], y);
+  float a = 1.f, b = 0.f;
+  if (AFFINE) { a = scale[c]; b = shift[c]; }
+  const int n = Ho * W;
+  double run_n = 0.0, run_mean = 0.0, run_m2 = 0.0;  // block-uniform (STATS only)
+
+  for (int base = 0; base < n; base += EPT * kThreads) {
+    float v[EPT];
+    Walker pos(base + threadIdx.x, kThreads, W);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int o = base + e * kThreads + threadIdx.x;
+      v[e] = 0.f;
+      if (o < n) {
+        const int r1 = pos.h * stride + g.y1;
+        const int c1 = pos.w + g.x1;
+        const bool rv1 = (unsigned)r1 < (unsigned)Hb, rv2 = (unsigned)(r1 + 1) < (unsigned)Hb;
+        const bool cv1 = (unsigned)c1 < (unsigned)W, cv2 = (unsigned)(c1 + 1) < (unsigned)W;
+        const float* p = src + (ptrdiff_t)r1 * W + c1;
+        const float q11 = tap<AFFINE>(p, rv1 && cv1, a, b);
+        const float q21 = tap<AFFINE>(p + 1, rv1 && cv2, a, b);
+        const float q12 = tap<AFFINE>(p + W, rv2 && cv1, a, b);
+        const float q22 = tap<AFFINE>(p + W + 1, rv2 && cv2, a, b);
+        v[e] = blend(q11, q21, q12, q22, g.dx, g.dy);
+        dst[o] = v[e];
+      }
+      pos.next();
+    }
+    if (STATS) {
+      const int cnt = min(n - base, EPT * kThreads);
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) s += v[e];  // invalid slots hold 0
+      s = block_sum(s, red);
+      const float mean = s / (float)cnt;
+      float m2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        const int o = base + e * kThreads + threadIdx.x;
+        const float d = v[e] - mean;
+        m2 += (o < n) ? d * d : 0.f;
+      }
+      m2 = block_sum(m2, red);
+      const Moments m = merge({run_n, run_mean, run_m2}, {(double)cnt, (double)mean, (double)m2});
+      run_n = m.n;
+      run_mean = m.mean;
+      run_m2 = m.m2;
+    }
+  }
+  if (STATS && threadIdx.x == 0) pstats[plane] = make_float2((float)run_mean, (float)run_m2);
+}
+
+// ------------------------------------------------------------------------------------
+// backward: input gradient (reverse shift) + position-gradient plane partials
+// ------------------------------------------------------------------------------------
+template <int EPT, bool AFFINE, bool RELU_MASK, int STRIDE>
+__global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
+    const float* __restrict__ gout, const float* __restrict__ in,
+    const float* __restrict__ xpos, const float* __restrict__ ypos,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    float* __restrict__ gin, float2* __restrict__ pgrad, int C, int Hb, int W, int Ho) {
+  __shared__ float red[2 * kThreads / 64];
+  const int plane = blockIdx.x;
+  const int c = plane % C;
+  const float* __restrict__ go = gout + (size_t)plane * Ho * W;
+  const float* __restrict__ src = in + (size_t)plane * Hb * W;
+  float* __restrict__ gi = gin + (size_t)plane * Hb * W;
+  const float x = xpos[c];
+  const float y = STRIDE == 1 ? ypos[c] : ypos[c] + 0.5f;
+  float a = 1.f, b = 0.f;
+  if (AFFINE) { a = scale[c]; b = shift[c]; }
+
+  // (1) grad_input over the bottom grid: bilinear sample of grad_output at (-x, -y)
+  //     (.cu:108-150 stride 1; .cu:191-254 stride 2 with the even-row rule)
+  {
+    const Geom r = make_geom(-x, -y);
+    const int nb = Hb * W;
+    for (int base = 0; base < nb; base += EPT * kThreads) {
+      Walker pos(base + threadIdx.x, kThreads, W);
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        const int o = base + e * kThreads + threadIdx.x;
+        if (o < nb) {
+          const int h1 = pos.h + r.y1, h2 = h1 + 1;
+          const int w1 = pos.w + r.x1, w2 = w1 + 1;
+          const bool cv1 = (unsigned)w1 < (unsigned)W, cv2 = (unsigned)w2 < (unsigned)W;
+          float q11 = 0.f, q21 = 0.f, q12 = 0.f, q22 = 0.f;
+          if (STRIDE == 1) {
+            const bool rv1 = (unsigned)h1 < (unsigned)Ho, rv2 = (unsigned)h2 < (unsigned)Ho;
+            const float* p = go + (ptrdiff_t)h1 * W + w1;
+            if (rv1 && cv1) q11 = p[0];
+            if (rv1 && cv2) q21 = p[1];
+            if (rv2 && cv1) q12 = p[W];
+            if (rv2 && cv2) q22 = p[W + 1];
+          } else {
+            // h_im % 2 == 0 (C++ remainder), then h_im / 2 (truncation), bounds on top grid
+            if (h1 % 2 == 0) {
+              const int hq = h1 / 2;
+              const bool rv = hq >= 0 && hq < Ho;
+              if (rv && cv1) q11 = go[hq * W + w1];
+              if (rv && cv2) q21 = go[hq * W + w2];
+            }
+            if (h2 % 2 == 0) {
+              const int hq = h2 / 2;
+              const bool rv = hq >= 0 && hq < Ho;
+              if (rv && cv1) q12 = go[hq * W + w1];
+              if (rv && cv2) q22 = go[hq * W + w2];
+            }
+          }
+          float val = blend(q11, q21, q12, q22, r.dx, r.dy);
+          if (RELU_MASK) val = src[o] > 0.f ? val : 0.f;
+          gi[o] = val;
+        }
+        pos.next();
+      }
+    }
+  }
+
+  // (2) position gradients over the top grid (.cu:321-349), summed over the plane
+  float ax = 0.f, ay = 0.f;
+  {
+    const Geom g = make_geom(x, y);
+    const int nt = Ho * W;
+    for (int base = 0; base < nt; base += EPT * kThreads) {
+      Walker pos(base + threadIdx.x, kThreads, W);
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        const int o = base + e * kThreads + threadIdx.x;
+        if (o < nt) {
+          const int r1 = pos.h * STRIDE + g.y1;
+          const int c1 = pos.w + g.x1;
+          const bool rv1 = (unsigned)r1 < (unsigned)Hb, rv2 = (unsigned)(r1 + 1) < (unsigned)Hb;
+          const bool cv1 = (unsigned)c1 < (unsigned)W, cv2 = (unsigned)(c1 + 1) < (unsigned)W;
+          const float* p = src + (ptrdiff_t)r1 * W + c1;
+          const float q11 = tap<AFFINE>(p, rv1 && cv1, a, b);
+          const float q21 = tap<AFFINE>(p + 1, rv1 && cv2, a, b);
+          const float q12 = tap<AFFINE>(p + W, rv2 && cv1, a, b);
+          const float q22 = tap<AFFINE>(p + W + 1, rv2 && cv2, a, b);
+          const float vx = (1.f - g.dy) * (q21 - q11) + g.dy * (q22 - q12);
+          const float vy = (1.f - g.dx) * (q12 - q11) + g.dx * (q22 - q21);
+          const float gv = go[o];
+          ax += vx * gv;
+          ay += vy * gv;
+        }
+        pos.next();
+      }
+    }
+  }
+  block_sum2(ax, ay, red);
+  if (threadIdx.x == 0) pgrad[plane] = make_float2(ax, ay);
+}
+
+// mean over the batch of the per-plane sums (== mean_b then sum_w, sum_h of .cu:501-509
+// up to rounding), then applyShiftConstraint (.cu:370-395) with its float/double
+// promotions: sqrt(dy*dy) in float (correctly rounded), quotients in float, times the
+// double literals 0.0 / 0.01, stored as float; the dr == 0 branch stores 0.0 / 0.0001.
+__global__ void tshift_pos_finalize_kernel(const float2* __restrict__ pgrad, int B, int C,
+                                           float* __restrict__ gx, float* __restrict__ gy) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sx = 0.0, sy = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const float2 p = pgrad[(size_t)b * C + c];
+    sx += (double)p.x;
+    sy += (double)p.y;
+  }
+  const float Gx = (float)(sx / (double)B);
+  const float Gy = (float)(sy / (double)B);
+  const float gy2 = Gy * Gy;
+  const float dr = (float)sqrt((double)gy2);
+  if (dr != 0.f) {
+    const float qx = (float)((double)Gx / (double)dr);
+    const float qy = (float)((double)Gy / (double)dr);
+    gx[c] = (float)((double)qx * 0.0);
+    gy[c] = (float)((double)qy * 0.01);
+  } else {
+    gx[c] = 0.0f;
+    gy[c] = (float)0.0001;
+  }
+}
+
+template <int EPT>
+void launch_fwd(bool affine, bool stats, const float* in, float* out, const float* xpos,
+                const float* ypos, const float* scale, const float* shift, float2* ps, int B,
+                int C, int H, int W, int Ho, int stride, hipStream_t st) {
+  dim3 grid(B * C), block(kThreads);
+#define SGCN_FWD(A, S)                                                                     \
+  tshift_fwd_kernel<EPT, A, S><<<grid, block, 0, st>>>(in, out, xpos, ypos, scale, shift, \
+                                                      ps, C, H, W, Ho, stride)
+  if (affine) {
+    if (stats) SGCN_FWD(true, true); else SGCN_FWD(true, false);
+  } else {
+    if (stats) SGCN_FWD(false, true); else SGCN_FWD(false, false);
+  }
+#undef SGCN_FWD
+}
+
+template <int EPT, int STRIDE>
+void launch_bwd(bool affine, bool relu, const float* gout, const float* in, const float* xpos,
+                const float* ypos, const float* scale, const float* shift, float* gin,
+                float2* pg, int B, int C, int H, int W, int Ho, hipStream_t st) {
+  dim3 grid(B * C), block(kThreads);
+#define SGCN_BWD(A, R)                                                                      \
+  tshift_bwd_kernel<EPT, A, R, STRIDE><<<grid, block, 0, st>>>(gout, in, xpos, ypos, scale, \
+                                                               shift, gin, pg, C, H, W, Ho)
+  if (affine) {
+    if (relu) SGCN_BWD(true, true); else SGCN_BWD(true, false);
+  } else {
+    if (relu) SGCN_BWD(false, true); else SGCN_BWD(false, false);
+  }
+#undef SGCN_BWD
+}
+
+int pick_ept(int n) {
+  const int per = (n + kThreads - 1) / kThreads;
+  return per <= 8 ? 8 : (per <= 16 ? 16 : 32);
+}
+
+}  // namespace
+}  // namespace sgcn
+
+using namespace sgcn;
+
+extern "C" {
+
+int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float* ypos,
+                    const float* in_scale, const float* in_shift, float* plane_stats, int B,
+                    int C, int H, int W, int stride, void* stream) {
+  SGCN_REQUIRE(B >= 0 && C > 0 && H >= 0 && W > 0 && stride >= 1);
+  SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
+  const int Ho = H / stride;
+  if (B == 0 || Ho == 0) return 0;
+  SGCN_REQUIRE(in && out && xpos && ypos);
+  SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  const bool aff = in_scale != nullptr, stats = plane_stats != nullptr;
+  float2* ps = (float2*)plane_stats;
+  switch (pick_ept(Ho * W)) {
+    case 8: launch_fwd<8>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, st); break;
+    case 16: launch_fwd<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, st); break;
+    default: launch_fwd<32>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, st); break;
+  }
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+size_t sgcn_tshift_bwd_ws_bytes(int B, int C) { return (size_t)B * C * sizeof(float2); }
+
+int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const float* ypos,
+                    const float* in_scale, const float* in_shift, int relu_mask, float* gin,
+                    float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
+                    int W, int stride, void* stream) {
+  SGCN_REQUIRE(B > 0 && C > 0 && H >= 0 && W > 0 && (stride == 1 || stride == 2));
+  SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
+  SGCN_REQUIRE(gout && in && xpos && ypos && gin && gx && gy && ws);
+  SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
+  SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
+  const int Ho = H / stride;
+  hipStream_t st = (hipStream_t)stream;
+  const bool aff = in_scale != nullptr, relu = relu_mask != 0;
+  float2* pg = (float2*)ws;
+  const int ept = pick_ept(H * W);
+#define SGCN_BWD_EPT(E)                                                                     \
+  (stride == 1 ? launch_bwd<E, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, gin, \
+                                  pg, B, C, H, W, Ho, st)                                   \
+               : launch_bwd<E, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, gin, \
+                                  pg, B, C, H, W, Ho, st))
+  if (ept == 8) SGCN_BWD_EPT(8); else if (ept == 16) SGCN_BWD_EPT(16); else SGCN_BWD_EPT(32);
+#undef SGCN_BWD_EPT
+  SGCN_LAUNCH_CHECK();
+  tshift_pos_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(pg, B, C, gx, gy);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

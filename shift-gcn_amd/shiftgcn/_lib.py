@@ -1,0 +1,66 @@
+"""Loader for the in-tree gfx950 HIP library (``libshiftgcn_hip.so``) behind
+``include/shiftgcn.h``.
+
+The product path has NO CPU or eager fallback: if the library is missing, or a tensor
+is not on a ROCm device, calls raise. ``torch`` is imported first so that the HIP
+runtime it already loaded (soname ``libamdhip64.so.7``) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen: one HIP runtime per process)
+
+LIB_NAME = "libshiftgcn_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+ABI_VERSION = 1
+EINVAL = -22
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_Z = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/shiftgcn.h
+SIGNATURES = {
+    "sgcn_abi_version": (_I, []),
+    "sgcn_tshift_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "sgcn_tshift_bwd_ws_bytes": (_Z, [_I, _I]),
+    "sgcn_tshift_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _Z, _I, _I, _I, _I,
+                             _I, _P]),
+}
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def load():
+    """Return the loaded ctypes library; raise NativeLibraryError when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (or `make -C shift-gcn_amd/csrc`). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.sgcn_abi_version() != ABI_VERSION:
+        raise NativeLibraryError("libshiftgcn_hip.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, name: str) -> None:
+    if rc == 0:
+        return
+    if rc == EINVAL:
+        raise ValueError(f"{name}: invalid argument (shape/pointer/stride)")
+    raise RuntimeError(f"{name}: HIP error {rc}")

@@ -1,0 +1,54 @@
+"""C-ABI library: loads, exports every symbol declared in include/shiftgcn.h, rejects bad
+arguments without touching the GPU (CPU-only checks)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "shiftgcn.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sgcn_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "sgcn_tshift_fwd" in syms and "sgcn_tshift_bwd" in syms
+    assert len(syms) >= 4
+
+
+def test_library_exports_every_declared_symbol():
+    from shiftgcn import _lib
+    lib = _lib.load()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    assert set(declared_symbols()) <= set(_lib.SIGNATURES), "ctypes signatures out of date"
+    assert lib.sgcn_abi_version() == _lib.ABI_VERSION
+
+
+def test_invalid_arguments_rejected_before_launch():
+    from shiftgcn import _lib
+    lib = _lib.load()
+    # NULL pointers / bad stride / mismatched affine: EINVAL, nothing enqueued
+    assert lib.sgcn_tshift_fwd(None, None, None, None, None, None, None, 2, 3, 4, 5, 1,
+                               None) == _lib.EINVAL
+    assert lib.sgcn_tshift_fwd(None, None, None, None, None, None, None, 2, 3, 4, 5, 0,
+                               None) == _lib.EINVAL
+    assert lib.sgcn_tshift_bwd(None, None, None, None, None, None, 0, None, None, None, None,
+                               0, 2, 3, 4, 5, 3, None) == _lib.EINVAL
+    assert lib.sgcn_tshift_bwd_ws_bytes(4, 8) == 4 * 8 * 8
+
+
+def test_cpu_tensor_raises_like_reference():
+    import torch
+    from shiftgcn import ShiftFunction
+    x = torch.zeros(1, 2, 4, 3)
+    p = torch.zeros(2)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        ShiftFunction.apply(x, p, p, 1)

@@ -1,0 +1,139 @@
+"""GPU parity: HIP temporal shift vs the oracle restatement of shift_cuda_kernel.cu.
+
+Bit-exact for forward / input gradient / position gradients at sizes the oracle runs in
+seconds and on the committed golden fixtures; size-independent properties (exact
+integer-shift translation, adjoint identity) at the full NTU plane size.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import shift_oracle as so
+from gen_fixtures import SHIFT_CASES, shift_case_inputs
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _run(x, xpos, ypos, stride, g):
+    from shiftgcn import ShiftFunction
+    xd = x.to(DEV).requires_grad_(True)
+    xp = xpos.to(DEV).requires_grad_(True)
+    yp = ypos.to(DEV).requires_grad_(True)
+    y = ShiftFunction.apply(xd, xp, yp, stride)
+    y.backward(g.to(DEV))
+    torch.cuda.synchronize()
+    return (y.detach().cpu().numpy(), xd.grad.cpu().numpy(), xp.grad.cpu().numpy(),
+            yp.grad.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", SHIFT_CASES, ids=[c[0] for c in SHIFT_CASES])
+def test_shift_matches_golden_bit_exact(golden, case):
+    fx = golden("shift_fixtures.npz")
+    name, B, C, H, W, stride = case
+    x, g, xpos, ypos = shift_case_inputs(*case)
+    out, gin, gx, gy = _run(x, xpos, ypos, stride, g)
+    assert np.array_equal(out, fx[f"shift_{name}_out"])
+    assert np.array_equal(gin, fx[f"shift_{name}_gin"])
+    assert np.array_equal(gx, fx[f"shift_{name}_gx"])
+    assert np.array_equal(gy, fx[f"shift_{name}_gy"])
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("shape", [(2, 64, 300, 25), (3, 16, 75, 33), (1, 5, 1, 25),
+                                   (2, 3, 301, 25)])
+def test_shift_matches_oracle_bit_exact(shape, stride):
+    B, C, H, W = shape
+    rng = np.random.default_rng(B * 1000 + C * 10 + H + stride)
+    x = rng.standard_normal(shape).astype(np.float32)
+    xpos = (rng.uniform(-1e-8, 1e-8, C)).astype(np.float32)
+    ypos = rng.uniform(-3.5, 3.5, C).astype(np.float32)
+    ypos[0] = 0.0
+    if C > 3:
+        xpos[1], xpos[2], ypos[2] = 1.5, -2.25, -float(H) - 1.0
+    g = rng.standard_normal((B, C, H // stride, W)).astype(np.float32)
+    out, gin, gx, gy = _run(torch.from_numpy(x), torch.from_numpy(xpos),
+                            torch.from_numpy(ypos), stride, torch.from_numpy(g))
+    ye = so.effective_ypos(ypos, stride)
+    assert np.array_equal(out, so.shift_forward(x, xpos, ye, stride))
+    rgin, rgx, rgy = so.shift_backward(g, x, xpos, ye, stride)
+    assert np.array_equal(gin, rgin)
+    assert np.array_equal(gx, rgx)
+    assert np.array_equal(gy, rgy)
+
+
+def test_full_size_integer_shift_is_exact_translation():
+    """NTU l2 plane shape at bs=8 clips (B=16): integer ypos -> exact translation."""
+    from shiftgcn import ops
+    B, C, H, W = 16, 64, 300, 25
+    x = torch.randn(B, C, H, W, device=DEV)
+    k = torch.randint(-5, 6, (C,), device=DEV).float()
+    xpos = torch.zeros(C, device=DEV)
+    y = ops.tshift_fwd(x, xpos, k, 1)
+    ref = torch.zeros_like(x)
+    for c in range(C):
+        s = int(k[c].item())
+        if s >= 0:
+            ref[:, c, :H - s] = x[:, c, s:]
+        else:
+            ref[:, c, -s:] = x[:, c, :H + s]
+    assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_full_size_adjoint_identity(stride):
+    from shiftgcn import ops
+    B, C, H, W = 32, 64, 300, 25
+    x = torch.randn(B, C, H, W, device=DEV)
+    xpos = (torch.rand(C, device=DEV) - 0.5) * 2e-8
+    ypos = (torch.rand(C, device=DEV) - 0.5) * 6
+    y = ops.tshift_fwd(x, xpos, ypos, stride)
+    g = torch.randn_like(y)
+    gin, _, _ = ops.tshift_bwd(g, x, xpos, ypos, stride)
+    lhs = (y.double() * g.double()).sum().item()
+    rhs = (x.double() * gin.double()).sum().item()
+    assert abs(lhs - rhs) <= 1e-5 * max(1.0, abs(lhs)) + 1e-2
+
+
+def test_fused_affine_and_stats_and_relu_mask():
+    """The Shift_tcn fusions: BN-affine on input taps, output plane moments, ReLU mask."""
+    from shiftgcn import ops
+    B, C, H, W = 4, 16, 40, 25
+    torch.manual_seed(0)
+    x = torch.randn(B, C, H, W, device=DEV)
+    a = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    xpos = (torch.rand(C, device=DEV) - 0.5) * 2e-8
+    ypos = (torch.rand(C, device=DEV) - 0.5) * 4
+    stats = torch.empty(B * C * 2, device=DEV)
+    y = ops.tshift_fwd(x, xpos, ypos, 1, scale=a, shift=b, stats=stats)
+    xa = x * a[None, :, None, None] + b[None, :, None, None]
+    y_ref = ops.tshift_fwd(xa.contiguous(), xpos, ypos, 1)
+    torch.testing.assert_close(y, y_ref, rtol=1e-6, atol=1e-6)
+    st = stats.view(B, C, 2).double()
+    yd = y.double().view(B, C, -1)
+    torch.testing.assert_close(st[..., 0], yd.mean(-1), rtol=1e-5, atol=1e-6)
+    m2 = ((yd - yd.mean(-1, keepdim=True)) ** 2).sum(-1)
+    torch.testing.assert_close(st[..., 1], m2, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(y)
+    gin, gx, gy = ops.tshift_bwd(g, x, xpos, ypos, 1, scale=a, shift=b)
+    gin_r, gx_r, gy_r = ops.tshift_bwd(g, xa.contiguous(), xpos, ypos, 1)
+    assert torch.equal(gin, gin_r)
+    assert torch.equal(gy, gy_r) and torch.equal(gx, gx_r)
+    r = torch.relu(torch.randn(B, C, H, W, device=DEV))
+    gin_m, _, _ = ops.tshift_bwd(g, r, xpos, ypos, 1, relu_mask=True)
+    gin_u, _, _ = ops.tshift_bwd(g, r, xpos, ypos, 1)
+    assert torch.equal(gin_m, torch.where(r > 0, gin_u, torch.zeros_like(gin_u)))
+
+
+def test_deterministic_position_grads():
+    from shiftgcn import ops
+    B, C, H, W = 64, 64, 300, 25
+    x = torch.randn(B, C, H, W, device=DEV)
+    g = torch.randn(B, C, H, W, device=DEV)
+    xpos = torch.zeros(C, device=DEV)
+    ypos = (torch.rand(C, device=DEV) - 0.5) * 2
+    r1 = ops.tshift_bwd(g, x, xpos, ypos, 1)
+    r2 = ops.tshift_bwd(g, x, xpos, ypos, 1)
+    for a_, b_ in zip(r1, r2):
+        assert torch.equal(a_, b_)
