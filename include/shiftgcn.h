@@ -66,6 +66,107 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
                     float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                     int W, int stride, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Pointwise (1x1) channel contraction with the joint-shift gathers fused (fp32 MFMA)
+ * ------------------------------------------------------------------------------------
+ * Plane operand addressing: element (b, ch, n), n = t*V + v, of a plane tensor lives at
+ *   ptr[b*bstride + ch*cstride + (t*tstride)*V + ((v + rsign*ch) mod V)]
+ * rsign = +1 is Shift_gcn's shift_in gather x[:, (v+c) mod V] (shift_gcn.py:108-112,127);
+ * as an OUTPUT mapping rsign = +1 stores y[d, t, v] at ((v+d) mod V), which is the
+ * shift_out gather z[v] = y[(v-d) mod V] (shift_gcn.py:114-118,136). tstride = 2 is the
+ * strided residual conv (shift_gcn.py:35-36). */
+
+/* Y[b][m][out(n,m)] (+)= act( sum_k A[m][k] * X'(b,k,n) + bias[m] ),  n < T*V
+ * A = w: w_mcontig ? w[k*M + m] : w[m*K + k];  X'(b,k,n) = X(b,k,n) * (mask ? mask[v*K+k] : 1)
+ * relu != 0 applies ReLU; accumulate != 0 adds into Y. K <= 256.
+ * Forward of Shift_gcn (einsum + Linear_bias, shift_gcn.py:131-132, w = Linear_weight
+ *   (C_in, C_out) m-contiguous, mask = tanh(Feature_Mask)+1), of Shift_tcn.temporal_linear
+ *   (:62,69) and the down/residual convs (:84, :35); with w transposed it is their dX. */
+int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x,
+                long long x_bstride, long long x_cstride, int x_tstride, int x_rsign,
+                const float* mask, float* y, long long y_bstride, long long y_cstride,
+                int y_tstride, int y_rsign, int relu, int accumulate, int B, int M, int K,
+                int T, int V, void* stream);
+
+/* Workspace bytes for sgcn_pw_dw. */
+size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V);
+
+/* Weight gradient over every position: dW[m][c] (+)= sum_{b,n} G(b,m,n) * X'(b,c,n)
+ * (stored [c][m] when dw_transpose, e.g. Linear_weight's (C_in, C_out) layout) and
+ * dbias[m] (+)= sum_{b,n} G(b,m,n) (dbias may be NULL). Deterministic split-K. */
+int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_tstride,
+               int g_rsign, const float* x, long long x_bstride, long long x_cstride,
+               int x_tstride, int x_rsign, const float* mask, float* dw, int dw_transpose,
+               int dw_accumulate, float* dbias, int dbias_accumulate, void* ws,
+               size_t ws_bytes, int B, int M, int Nc, int T, int V, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Training-mode BatchNorm (shift_gcn.py:38,55-56,85,99,137) and unit tails
+ * ------------------------------------------------------------------------------------
+ * per_joint = 1: BatchNorm1d(V*C) over (n, t) of a (B, C, T, V) tensor, feature
+ * f = c*V + v here, reference feature index v*C + c (pass perm_V = V to finalize);
+ * per_joint = 0: BatchNorm2d, feature = channel. */
+
+/* Bytes of the per-(b, feature) partials written by sgcn_moments / sgcn_bn_bwd_reduce. */
+size_t sgcn_moments_ws_bytes(int B, int C, int V, int per_joint);
+
+/* part[b][f] = {mean, M2} of x over the plane (or over t per joint). */
+int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int per_joint,
+                 void* stream);
+
+/* Merge B partials (n_part elements each) per feature: batch mean / biased var ->
+ * mean, invstd, scale = gamma*invstd, shift = beta - mean*scale (all [F], local feature
+ * order); updates running_mean/var (momentum, unbiased var) and num_batches (+1) when
+ * non-NULL, in the reference feature order (perm_V > 0: per-joint mapping). */
+int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
+                     const float* gamma, const float* beta, float eps, float momentum,
+                     float* running_mean, float* running_var, long long* num_batches,
+                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+
+/* Eval-mode scale/shift from running statistics. */
+int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
+                      const float* running_mean, const float* running_var, float eps,
+                      float* scale, float* shift, void* stream);
+
+/* y = act(x*scale[f] + shift[f] + res), res = r*rscale[c] + rshift[c] (both given),
+ * r (rscale NULL) or 0 (r NULL); act = ReLU if relu. */
+int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
+                  const float* r, const float* rscale, const float* rshift, int relu,
+                  float* y, int B, int C, int T, int V, void* stream);
+
+/* Backward partials: g = dy * (relu ? y > 0 : 1); part[b][f] = {sum g, sum g*xhat};
+ * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none). */
+int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x,
+                       const float* mean, const float* invstd, int per_joint, const float* r,
+                       const float* rmean, const float* rinvstd, float* part, float* rpart,
+                       int B, int C, int T, int V, void* stream);
+
+/* dgamma/dbeta (+)= sums (reference feature order); coef[3][F] = {k1, k2, k3} such that
+ * dx = k1*g + k2*x + k3 (training-mode BatchNorm input gradient). */
+int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int perm_V,
+                         const float* mean, const float* invstd, const float* gamma,
+                         float* dgamma, float* dbeta, int accumulate, float* coef,
+                         void* stream);
+
+/* dx = k1*g + k2*x + k3; dr = g (rcoef NULL, dr given) or rk1*g + rk2*r + rk3. */
+int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
+                      const float* coef, int per_joint, const float* r, const float* rcoef,
+                      float* dx, float* dr, int B, int C, int T, int V, void* stream);
+
+/* m = tanh(Feature_Mask) + 1 (shift_gcn.py:129); n = V*C. */
+int sgcn_mask_prep(const float* mask, float* m, int n, void* stream);
+
+/* Shift_gcn input side of the backward: dx[b,c,t,v] = dxt[b,c,t,u]*m[u][c] + add1 + add2
+ * with u = (v - c) mod V (transpose of the shift_in gather); dmask_part[b][c][u] =
+ * sum_t dxt * x0 at the gathered position. add1/add2 may be NULL. */
+int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
+                       const float* add2, float* dx, float* dmask_part, int B, int C, int T,
+                       int V, void* stream);
+
+/* dmask[u][c] (+)= (sum_b dmask_part[b][c][u]) * (1 - tanh(mask[u][c])^2). */
+int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,
+                            float* dmask, int accumulate, void* stream);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -142,7 +142,7 @@ class Shift_gcn(nn.Module):  # noqa: N801
     """``shift_gcn.py:77-142``: joint shift-in gather, feature mask, C_in x C_out linear,
     bias, joint shift-out gather, BN1d(V*C_out), + down(x0), ReLU."""
 
-    def __init__(self, in_channels, out_channels, A=None, coff_embedding=4, num_subset=3,
+    def __init__(self, in_channels, out_channels, A, coff_embedding=4, num_subset=3,
                  num_point=25):
         super().__init__()
         self.in_channels = in_channels
@@ -187,7 +187,7 @@ class Shift_gcn(nn.Module):  # noqa: N801
 class TCN_GCN_unit(nn.Module):  # noqa: N801
     """``shift_gcn.py:145-162``: relu(tcn1(gcn1(x)) + residual(x))."""
 
-    def __init__(self, in_channels, out_channels, A=None, stride=1, residual=True,
+    def __init__(self, in_channels, out_channels, A, stride=1, residual=True,
                  num_point=25):
         super().__init__()
         self.gcn1 = Shift_gcn(in_channels, out_channels, A, num_point=num_point)

@@ -1,0 +1,526 @@
+// Training-mode BatchNorm and the elementwise unit tails of the Shift-GCN hot path.
+//
+// Reference semantics (model/shift_gcn.py): five BatchNorms per TCN_GCN_unit —
+//   gcn.bn   = BatchNorm1d(V*C_out) over (n*t) with feature f = v*C_out + d  (:99,:137)
+//   down.1, tcn.bn, tcn.bn2, residual.bn = BatchNorm2d over (n, t, v)         (:85,:55-56,:38)
+// each followed by the unit's residual add and ReLU (:140-141, :161-162).
+//
+// Layout stays (N·M, C, T, V). "per_joint" selects the BN1d-over-(d,v) feature set
+// (f = d*V + v here, mapped to the reference index v*D + d when reading/writing gamma,
+// beta and running stats); otherwise features are channels.
+//
+// Statistics are deterministic and numerically robust: per-(sample, feature) partial
+// moments (mean, M2) from one workgroup per (n·m, c) plane, merged in fixed order with
+// Chan's formula in double by the finalize kernels. Running stats follow PyTorch
+// (momentum 0.1, unbiased running variance, num_batches_tracked += 1).
+#include "common.hpp"
+
+namespace sgcn {
+namespace {
+
+constexpr int kThreads = 256;
+
+struct Welford {
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  __device__ __forceinline__ void add(float x) {
+    n += 1.f;
+    const float d = x - mean;
+    mean += d / n;
+    m2 += d * (x - mean);
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// forward statistics
+// ------------------------------------------------------------------------------------
+// part[plane] = {mean, M2} over the plane (per_joint = 0), or part[plane*V + v] over t.
+template <bool PER_JOINT>
+__global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restrict__ x,
+                                                            float2* __restrict__ part, int T,
+                                                            int V) {
+  __shared__ float sn[kThreads], sm[kThreads], s2[kThreads];
+  const int plane = blockIdx.x;
+  const int P = T * V;
+  const float* __restrict__ xp = x + (size_t)plane * P;
+  Welford w;
+  if (PER_JOINT) {
+    const int G = kThreads / V;  // row groups
+    const int i = threadIdx.x;
+    if (i < G * V) {
+      const int v = i % V, r = i / V;
+      for (int t = r; t < T; t += G) w.add(xp[t * V + v]);
+    }
+    sn[i] = w.n; sm[i] = w.mean; s2[i] = w.m2;
+    __syncthreads();
+    if (i < V) {
+      Moments m{0.0, 0.0, 0.0};
+      for (int g = 0; g < G; ++g) {
+        const int j = g * V + i;
+        m = merge(m, {(double)sn[j], (double)sm[j], (double)s2[j]});
+      }
+      part[(size_t)plane * V + i] = make_float2((float)m.mean, (float)m.m2);
+    }
+  } else {
+    for (int o = threadIdx.x; o < P; o += kThreads) w.add(xp[o]);
+    sn[threadIdx.x] = w.n; sm[threadIdx.x] = w.mean; s2[threadIdx.x] = w.m2;
+    __syncthreads();
+    // tree merge in float pairs then double at the top 64
+    for (int s = kThreads / 2; s >= 64; s >>= 1) {
+      if (threadIdx.x < s) {
+        const int j = threadIdx.x + s;
+        const Moments m = merge({(double)sn[threadIdx.x], (double)sm[threadIdx.x], (double)s2[threadIdx.x]},
+                                {(double)sn[j], (double)sm[j], (double)s2[j]});
+        sn[threadIdx.x] = (float)m.n; sm[threadIdx.x] = (float)m.mean; s2[threadIdx.x] = (float)m.m2;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      Moments m{0.0, 0.0, 0.0};
+      for (int j = 0; j < 64; ++j) m = merge(m, {(double)sn[j], (double)sm[j], (double)s2[j]});
+      part[plane] = make_float2((float)m.mean, (float)m.m2);
+    }
+  }
+}
+
+__device__ __forceinline__ int ref_feature(int f, int perm_V, int F) {
+  if (perm_V <= 0) return f;
+  const int D = F / perm_V;
+  const int d = f / perm_V, v = f - d * perm_V;
+  return v * D + d;  // BatchNorm1d(V*C) feature index of (d, v)  (shift_gcn.py:135-137)
+}
+
+// part layout [B][C][J] (J = V if per-joint else 1); feature f = c*J + j; each partial
+// covers n_part elements.
+__global__ void bn_finalize_kernel(const float2* __restrict__ part, int B, int F, int n_part,
+                                   int perm_V, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float eps, float momentum,
+                                   float* __restrict__ running_mean,
+                                   float* __restrict__ running_var,
+                                   long long* __restrict__ num_batches,
+                                   float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                   float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f == 0 && num_batches) *num_batches += 1;
+  if (f >= F) return;
+  Moments m{0.0, 0.0, 0.0};
+  for (int b = 0; b < B; ++b) {
+    const float2 p = part[(size_t)b * F + f];
+    m = merge(m, {(double)n_part, (double)p.x, (double)p.y});
+  }
+  const double var = m.n > 0 ? m.m2 / m.n : 0.0;
+  const float mean = (float)m.mean;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const int rf = ref_feature(f, perm_V, F);
+  const float g = gamma ? gamma[rf] : 1.f;
+  const float bb = beta ? beta[rf] : 0.f;
+  const float scale = g * invstd;
+  mean_out[f] = mean;
+  invstd_out[f] = invstd;
+  scale_out[f] = scale;
+  shift_out[f] = bb - mean * scale;
+  if (running_mean) {
+    const double unbiased = m.n > 1 ? m.m2 / (m.n - 1.0) : var;
+    running_mean[rf] = (1.f - momentum) * running_mean[rf] + momentum * mean;
+    running_var[rf] = (1.f - momentum) * running_var[rf] + momentum * (float)unbiased;
+  }
+}
+
+// eval-mode coefficients from running statistics
+__global__ void bn_eval_coef_kernel(int F, int perm_V, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta,
+                                    const float* __restrict__ running_mean,
+                                    const float* __restrict__ running_var, float eps,
+                                    float* __restrict__ scale_out,
+                                    float* __restrict__ shift_out) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  const int rf = ref_feature(f, perm_V, F);
+  const float invstd = (float)(1.0 / sqrt((double)running_var[rf] + (double)eps));
+  const float scale = (gamma ? gamma[rf] : 1.f) * invstd;
+  scale_out[f] = scale;
+  shift_out[f] = (beta ? beta[rf] : 0.f) - running_mean[rf] * scale;
+}
+
+// ------------------------------------------------------------------------------------
+// apply: y = act(x*scale[f] + shift[f] + res); res = r*rscale[c] + rshift[c] | r | 0
+// ------------------------------------------------------------------------------------
+template <bool PER_JOINT, int RES, bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ r,
+    const float* __restrict__ rscale, const float* __restrict__ rshift,
+    float* __restrict__ y, int C, int T, int V) {
+  const int plane = blockIdx.x, c = plane % C;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  float sc = 0.f, sh = 0.f, rsc = 1.f, rsh = 0.f;
+  if (!PER_JOINT) { sc = scale[c]; sh = shift[c]; }
+  if (RES == 2) { rsc = rscale[c]; rsh = rshift[c]; }
+  int v = threadIdx.x % V;
+  const int dv = kThreads % V;
+  for (int o = threadIdx.x; o < P; o += kThreads) {
+    float a = x[off + o];
+    if (PER_JOINT) a = a * scale[c * V + v] + shift[c * V + v];
+    else a = a * sc + sh;
+    if (RES == 1) a += r[off + o];
+    if (RES == 2) a += r[off + o] * rsc + rsh;
+    if (RELU) a = fmaxf(a, 0.f);
+    y[off + o] = a;
+    v += dv;
+    if (v >= V) v -= V;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// backward: reductions of g = dy*(y>0) and g*xhat per feature
+// ------------------------------------------------------------------------------------
+template <bool PER_JOINT, bool RELU, bool RESBN>
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ r, const float* __restrict__ rmean,
+    const float* __restrict__ rinvstd, float2* __restrict__ part,
+    float2* __restrict__ rpart, int C, int T, int V) {
+  __shared__ float s0[kThreads], s1[kThreads], red[2 * kThreads / 64];
+  const int plane = blockIdx.x, c = plane % C;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  float rm = 0.f, ri = 0.f;
+  if (RESBN) { rm = rmean[c]; ri = rinvstd[c]; }
+  float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+  if (PER_JOINT) {
+    const int G = kThreads / V;
+    const int i = threadIdx.x;
+    if (i < G * V) {
+      const int v = i % V, rr = i / V;
+      const float mu = mean[c * V + v], is = invstd[c * V + v];
+      for (int t = rr; t < T; t += G) {
+        const int o = t * V + v;
+        float g = dy[off + o];
+        if (RELU) g = y[off + o] > 0.f ? g : 0.f;
+        a0 += g;
+        a1 += g * ((x[off + o] - mu) * is);
+        if (RESBN) { b0 += g; b1 += g * ((r[off + o] - rm) * ri); }
+      }
+    }
+    if (RESBN) block_sum2(b0, b1, red);
+    s0[i] = a0; s1[i] = a1;
+    __syncthreads();
+    if (i < V) {
+      float t0 = 0.f, t1 = 0.f;
+      for (int g = 0; g < G; ++g) { t0 += s0[g * V + i]; t1 += s1[g * V + i]; }
+      part[(size_t)plane * V + i] = make_float2(t0, t1);
+    }
+    if (RESBN && i == 0) rpart[plane] = make_float2(b0, b1);
+  } else {
+    const float mu = mean[c], is = invstd[c];
+    for (int o = threadIdx.x; o < P; o += kThreads) {
+      float g = dy[off + o];
+      if (RELU) g = y[off + o] > 0.f ? g : 0.f;
+      a0 += g;
+      a1 += g * ((x[off + o] - mu) * is);
+      if (RESBN) { b0 += g; b1 += g * ((r[off + o] - rm) * ri); }
+    }
+    block_sum2(a0, a1, red);
+    if (RESBN) block_sum2(b0, b1, red);
+    if (threadIdx.x == 0) {
+      part[plane] = make_float2(a0, a1);
+      if (RESBN) rpart[plane] = make_float2(b0, b1);
+    }
+  }
+}
+
+// dgamma = sum g*xhat, dbeta = sum g; dx = k1*g + k2*x + k3 with
+// k1 = gamma*invstd, k2 = -k1*invstd*mean(g*xhat), k3 = -k1*mean(g) - k2*mean_x
+__global__ void bn_bwd_finalize_kernel(const float2* __restrict__ part, int B, int F,
+                                       float n_total, int perm_V,
+                                       const float* __restrict__ mean,
+                                       const float* __restrict__ invstd,
+                                       const float* __restrict__ gamma,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       int accumulate, float* __restrict__ coef) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const float2 p = part[(size_t)b * F + f];
+    sg += p.x;
+    sgx += p.y;
+  }
+  const int rf = ref_feature(f, perm_V, F);
+  if (dgamma) dgamma[rf] = accumulate ? dgamma[rf] + (float)sgx : (float)sgx;
+  if (dbeta) dbeta[rf] = accumulate ? dbeta[rf] + (float)sg : (float)sg;
+  const float g = gamma ? gamma[rf] : 1.f;
+  const float is = invstd[f];
+  const float k1 = g * is;
+  const float k2 = (float)(-(double)k1 * (double)is * (sgx / (double)n_total));
+  const float k3 = (float)(-(double)k1 * (sg / (double)n_total) - (double)k2 * (double)mean[f]);
+  coef[f] = k1;
+  coef[F + f] = k2;
+  coef[2 * F + f] = k3;
+}
+
+// dx = k1[f]*g + k2[f]*x + k3[f]; RES: 1 -> dr = g, 2 -> dr = rk1*g + rk2*r + rk3
+template <bool PER_JOINT, bool RELU, int RES>
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
+    const float* __restrict__ coef, int F, const float* __restrict__ r,
+    const float* __restrict__ rcoef, int RF, float* __restrict__ dx, float* __restrict__ dr,
+    int C, int T, int V) {
+  const int plane = blockIdx.x, c = plane % C;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  float k1 = 0.f, k2 = 0.f, k3 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+  if (!PER_JOINT) { k1 = coef[c]; k2 = coef[F + c]; k3 = coef[2 * F + c]; }
+  if (RES == 2) { q1 = rcoef[c]; q2 = rcoef[RF + c]; q3 = rcoef[2 * RF + c]; }
+  int v = threadIdx.x % V;
+  const int dv = kThreads % V;
+  for (int o = threadIdx.x; o < P; o += kThreads) {
+    float g = dy[off + o];
+    if (RELU) g = y[off + o] > 0.f ? g : 0.f;
+    if (PER_JOINT) {
+      const int f = c * V + v;
+      k1 = coef[f]; k2 = coef[F + f]; k3 = coef[2 * F + f];
+    }
+    dx[off + o] = k1 * g + k2 * x[off + o] + k3;
+    if (RES == 1) dr[off + o] = g;
+    if (RES == 2) dr[off + o] = q1 * g + q2 * r[off + o] + q3;
+    v += dv;
+    if (v >= V) v -= V;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Shift_gcn input-side backward: undo shift_in and the feature mask
+// ------------------------------------------------------------------------------------
+// dx[b,c,t,v'] = dxt[b,c,t,u]*m[u][c] (+ add1 + add2), u = (v' - c) mod V  (index_select^T)
+// dmask_part[b][c][u] = sum_t dxt[b,c,t,u] * x0[b,c,t,(u+c) mod V]
+__global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
+    const float* __restrict__ dxt, const float* __restrict__ x0, const float* __restrict__ m,
+    const float* __restrict__ add1, const float* __restrict__ add2, float* __restrict__ dx,
+    float* __restrict__ dmask_part, int C, int T, int V) {
+  __shared__ float s0[kThreads];
+  const int plane = blockIdx.x, c = plane % C;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  const int rc = c % V;
+  // scatter pass over destination positions v'
+  {
+    int v = threadIdx.x % V;
+    const int dv = kThreads % V;
+    for (int o = threadIdx.x; o < P; o += kThreads) {
+      int u = v - rc;
+      u = u < 0 ? u + V : u;
+      const int src = o - v + u;
+      float val = dxt[off + src] * m[u * C + c];
+      if (add1) val += add1[off + o];
+      if (add2) val += add2[off + o];
+      dx[off + o] = val;
+      v += dv;
+      if (v >= V) v -= V;
+    }
+  }
+  // mask-gradient partials per u over t
+  const int G = kThreads / V;
+  const int i = threadIdx.x;
+  float acc = 0.f;
+  if (i < G * V) {
+    const int u = i % V, rr = i / V;
+    int xv = u + rc;
+    xv = xv >= V ? xv - V : xv;
+    for (int t = rr; t < T; t += G) acc += dxt[off + t * V + u] * x0[off + t * V + xv];
+  }
+  s0[i] = acc;
+  __syncthreads();
+  if (i < V) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += s0[g * V + i];
+    dmask_part[(size_t)plane * V + i] = s;
+  }
+}
+
+// m = tanh(mask) + 1   (shift_gcn.py:129)
+__global__ void mask_prep_kernel(const float* __restrict__ mask, float* __restrict__ m, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) m[i] = tanhf(mask[i]) + 1.f;
+}
+
+// dmask[u][c] (+)= (sum_b part[b][c][u]) * (1 - tanh(mask)^2)
+__global__ void mask_grad_finalize_kernel(const float* __restrict__ part,
+                                          const float* __restrict__ mask, int B, int C, int V,
+                                          float* __restrict__ dmask, int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // i = u*C + c
+  if (i >= C * V) return;
+  const int u = i / C, c = i - u * C;
+  double s = 0.0;
+  for (int b = 0; b < B; ++b) s += part[((size_t)b * C + c) * V + u];
+  const float t = tanhf(mask[i]);
+  const float g = (float)s * (1.f - t * t);
+  dmask[i] = accumulate ? dmask[i] + g : g;
+}
+
+}  // namespace
+}  // namespace sgcn
+
+using namespace sgcn;
+
+#define SGCN_PLANE_CHECK() \
+  SGCN_REQUIRE(B >= 0 && C > 0 && T >= 0 && V > 0 && V <= kThreads)
+
+extern "C" {
+
+size_t sgcn_moments_ws_bytes(int B, int C, int V, int per_joint) {
+  return (size_t)B * C * (per_joint ? V : 1) * sizeof(float2);
+}
+
+int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int per_joint,
+                 void* stream) {
+  SGCN_PLANE_CHECK();
+  if (B == 0) return 0;
+  SGCN_REQUIRE(x && part && T > 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (per_joint) moments_kernel<true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V);
+  else moments_kernel<false><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
+                     const float* gamma, const float* beta, float eps, float momentum,
+                     float* running_mean, float* running_var, long long* num_batches,
+                     float* mean, float* invstd, float* scale, float* shift, void* stream) {
+  SGCN_REQUIRE(part && B > 0 && F > 0 && n_part > 0 && mean && invstd && scale && shift);
+  SGCN_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
+  SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  bn_finalize_kernel<<<(F + 255) / 256, 256, 0, st>>>(
+      (const float2*)part, B, F, n_part, perm_V, gamma, beta, eps, momentum, running_mean,
+      running_var, num_batches, mean, invstd, scale, shift);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
+                      const float* running_mean, const float* running_var, float eps,
+                      float* scale, float* shift, void* stream) {
+  SGCN_REQUIRE(F > 0 && running_mean && running_var && scale && shift);
+  SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
+  bn_eval_coef_kernel<<<(F + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      F, perm_V, gamma, beta, running_mean, running_var, eps, scale, shift);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
+                  const float* r, const float* rscale, const float* rshift, int relu,
+                  float* y, int B, int C, int T, int V, void* stream) {
+  SGCN_PLANE_CHECK();
+  if (B == 0 || T == 0) return 0;
+  SGCN_REQUIRE(x && scale && shift && y);
+  SGCN_REQUIRE((rscale == nullptr) == (rshift == nullptr) && (r || !rscale));
+  hipStream_t st = (hipStream_t)stream;
+  const int res = r == nullptr ? 0 : (rscale ? 2 : 1);
+  dim3 g(B * C);
+#define SGCN_APPLY(PJ, RS, RL) \
+  bn_apply_kernel<PJ, RS, RL><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale, rshift, y, C, T, V)
+#define SGCN_APPLY_R(PJ, RL) \
+  if (res == 0) SGCN_APPLY(PJ, 0, RL); else if (res == 1) SGCN_APPLY(PJ, 1, RL); else SGCN_APPLY(PJ, 2, RL)
+  if (per_joint) { if (relu) { SGCN_APPLY_R(true, true); } else { SGCN_APPLY_R(true, false); } }
+  else { if (relu) { SGCN_APPLY_R(false, true); } else { SGCN_APPLY_R(false, false); } }
+#undef SGCN_APPLY_R
+#undef SGCN_APPLY
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x,
+                       const float* mean, const float* invstd, int per_joint, const float* r,
+                       const float* rmean, const float* rinvstd, float* part, float* rpart,
+                       int B, int C, int T, int V, void* stream) {
+  SGCN_PLANE_CHECK();
+  SGCN_REQUIRE(B > 0 && T > 0 && dy && x && mean && invstd && part && (y || !relu));
+  SGCN_REQUIRE((r == nullptr) == (rpart == nullptr) && (!r || (rmean && rinvstd)));
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g(B * C);
+  const bool rb = r != nullptr;
+#define SGCN_RED(PJ, RL, RB)                                                            \
+  bn_bwd_reduce_kernel<PJ, RL, RB><<<g, kThreads, 0, st>>>(dy, y, x, mean, invstd, r, rmean, \
+                                                           rinvstd, (float2*)part,        \
+                                                           (float2*)rpart, C, T, V)
+  if (per_joint) {
+    if (relu) { if (rb) SGCN_RED(true, true, true); else SGCN_RED(true, true, false); }
+    else { if (rb) SGCN_RED(true, false, true); else SGCN_RED(true, false, false); }
+  } else {
+    if (relu) { if (rb) SGCN_RED(false, true, true); else SGCN_RED(false, true, false); }
+    else { if (rb) SGCN_RED(false, false, true); else SGCN_RED(false, false, false); }
+  }
+#undef SGCN_RED
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int perm_V,
+                         const float* mean, const float* invstd, const float* gamma,
+                         float* dgamma, float* dbeta, int accumulate, float* coef,
+                         void* stream) {
+  SGCN_REQUIRE(part && B > 0 && F > 0 && n_total > 0 && mean && invstd && coef);
+  SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
+  bn_bwd_finalize_kernel<<<(F + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      (const float2*)part, B, F, (float)n_total, perm_V, mean, invstd, gamma, dgamma, dbeta,
+      accumulate, coef);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
+                      const float* coef, int per_joint, const float* r, const float* rcoef,
+                      float* dx, float* dr, int B, int C, int T, int V, void* stream) {
+  SGCN_PLANE_CHECK();
+  if (B == 0 || T == 0) return 0;
+  SGCN_REQUIRE(dy && x && coef && dx && (y || !relu));
+  SGCN_REQUIRE(!rcoef || (r && dr));
+  hipStream_t st = (hipStream_t)stream;
+  const int res = dr == nullptr ? 0 : (rcoef ? 2 : 1);
+  const int F = per_joint ? C * V : C;
+  dim3 g(B * C);
+#define SGCN_BA(PJ, RL, RS) \
+  bn_bwd_apply_kernel<PJ, RL, RS><<<g, kThreads, 0, st>>>(dy, y, x, coef, F, r, rcoef, C, dx, dr, C, T, V)
+#define SGCN_BA_R(PJ, RL) \
+  if (res == 0) SGCN_BA(PJ, RL, 0); else if (res == 1) SGCN_BA(PJ, RL, 1); else SGCN_BA(PJ, RL, 2)
+  if (per_joint) { if (relu) { SGCN_BA_R(true, true); } else { SGCN_BA_R(true, false); } }
+  else { if (relu) { SGCN_BA_R(false, true); } else { SGCN_BA_R(false, false); } }
+#undef SGCN_BA_R
+#undef SGCN_BA
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_mask_prep(const float* mask, float* m, int n, void* stream) {
+  SGCN_REQUIRE(mask && m && n > 0);
+  mask_prep_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(mask, m, n);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
+                       const float* add2, float* dx, float* dmask_part, int B, int C, int T,
+                       int V, void* stream) {
+  SGCN_PLANE_CHECK();
+  if (B == 0 || T == 0) return 0;
+  SGCN_REQUIRE(dxt && x0 && m && dx && dmask_part);
+  gcn_dx_finish_kernel<<<B * C, kThreads, 0, (hipStream_t)stream>>>(dxt, x0, m, add1, add2, dx,
+                                                                    dmask_part, C, T, V);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,
+                            float* dmask, int accumulate, void* stream) {
+  SGCN_REQUIRE(part && mask && dmask && B > 0 && C > 0 && V > 0);
+  mask_grad_finalize_kernel<<<(C * V + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      part, mask, B, C, V, dmask, accumulate);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

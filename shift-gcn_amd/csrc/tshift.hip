@@ -348,10 +348,11 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
                     int W, int stride, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H >= 0 && W > 0 && (stride == 1 || stride == 2));
   SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
-  SGCN_REQUIRE(gout && in && xpos && ypos && gin && gx && gy && ws);
+  const int Ho = H / stride;
+  SGCN_REQUIRE((gout || Ho == 0) && (in || H == 0) && (gin || H == 0));
+  SGCN_REQUIRE(xpos && ypos && gx && gy && ws);
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
   SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
-  const int Ho = H / stride;
   hipStream_t st = (hipStream_t)stream;
   const bool aff = in_scale != nullptr, relu = relu_mask != 0;
   float2* pg = (float2*)ws;

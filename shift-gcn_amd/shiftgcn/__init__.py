@@ -5,5 +5,8 @@ Drop-in module surface of the reference (``model/shift_gcn.py``,
 (``shift-gcn_amd/csrc``) behind the C ABI ``include/shiftgcn.h``.
 """
 from .shift import Shift, ShiftFunction  # noqa: F401
+from .shift_gcn import (Model, Shift_gcn, Shift_tcn, TCN_GCN_unit, bn_init,  # noqa: F401
+                        conv_init, import_class, tcn)
 
-__all__ = ["Shift", "ShiftFunction"]
+__all__ = ["Shift", "ShiftFunction", "Model", "Shift_gcn", "Shift_tcn", "TCN_GCN_unit", "tcn",
+           "import_class", "conv_init", "bn_init"]

@@ -23,6 +23,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
 _Z = ctypes.c_size_t
+_L = ctypes.c_longlong
 
 # name -> (restype, argtypes); mirrors include/shiftgcn.h
 SIGNATURES = {
@@ -31,6 +32,24 @@ SIGNATURES = {
     "sgcn_tshift_bwd_ws_bytes": (_Z, [_I, _I]),
     "sgcn_tshift_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _Z, _I, _I, _I, _I,
                              _I, _P]),
+    "sgcn_pw_fwd": (_I, [_P, _I, _P, _P, _L, _L, _I, _I, _P, _P, _L, _L, _I, _I, _I, _I, _I,
+                         _I, _I, _I, _I, _P]),
+    "sgcn_pw_dw_ws_bytes": (_Z, [_I, _I, _I, _I, _I]),
+    "sgcn_pw_dw": (_I, [_P, _L, _L, _I, _I, _P, _L, _L, _I, _I, _P, _P, _I, _I, _P, _I, _P, _Z,
+                        _I, _I, _I, _I, _I, _P]),
+    "sgcn_moments_ws_bytes": (_Z, [_I, _I, _I, _I]),
+    "sgcn_moments": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "sgcn_bn_finalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P,
+                              _P]),
+    "sgcn_bn_eval_coef": (_I, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P]),
+    "sgcn_bn_apply": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P]),
+    "sgcn_bn_bwd_reduce": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I,
+                                _P]),
+    "sgcn_bn_bwd_finalize": (_I, [_P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _I, _P, _P]),
+    "sgcn_bn_bwd_apply": (_I, [_P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "sgcn_mask_prep": (_I, [_P, _P, _I, _P]),
+    "sgcn_gcn_dx_finish": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "sgcn_mask_grad_finalize": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
 }
 
 

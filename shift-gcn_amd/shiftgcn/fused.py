@@ -1,0 +1,352 @@
+"""Fused forward/backward recipes of the Shift-GCN blocks on the HIP library.
+
+Each block of ``model/shift_gcn.py`` is computed by a short, fixed sequence of C-ABI
+launches (no torch compute ops), with its backward written out explicitly so that the
+fusions survive training:
+
+Shift_gcn (shift_gcn.py:121-142)
+  fwd : mask_prep -> pw_fwd[shift_in gather + mask + einsum + bias + shift_out scatter]
+        -> moments(per joint) -> bn_finalize -> [down: pw_fwd -> moments -> finalize]
+        -> bn_apply(+down/identity, ReLU)
+  bwd : bn_bwd_reduce(ReLU mask, both BNs) -> finalize x2 -> bn_bwd_apply
+        -> pw_dw(Linear_weight^T, bias) -> pw_fwd(dX in gathered space)
+        -> gcn_dx_finish(shift_in^T + mask, dmask partials) -> mask_grad_finalize
+        -> [down: pw_dw, pw_fwd(accumulate)]
+Shift_tcn (shift_gcn.py:65-74)
+  fwd : moments -> finalize(bn) -> tshift_fwd[bn affine fused on taps]
+        -> pw_fwd[temporal_linear + bias + ReLU] -> tshift_fwd[stride s, bn2 moments fused]
+        -> finalize(bn2) -> (standalone: bn_apply)
+  bwd : tshift_bwd[ReLU mask fused] -> pw_dw -> pw_fwd(dX) -> tshift_bwd[bn affine]
+        -> bn_bwd_reduce -> finalize -> bn_bwd_apply
+TCN_GCN_unit (shift_gcn.py:160-162): bn2 apply + residual (0 / identity / tcn conv+BN) +
+  ReLU is ONE bn_apply launch; its backward ONE reduce + ONE apply.
+
+Everything runs on torch's current stream; intermediate buffers come from torch's
+caching allocator, so a whole training step can be captured in a hipGraph.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from .ops import PlaneView as PV
+
+
+def _empty(*shape, like):
+    return torch.empty(shape, device=like.device, dtype=torch.float32)
+
+
+# ======================================================================================
+# Shift_gcn
+# ======================================================================================
+class GcnSaved:
+    __slots__ = ("x0", "Z", "zst", "D0", "dst", "H", "m")
+
+
+def gcn_forward(mod, x0, training):
+    B, Cin, T, V = x0.shape
+    Cout = mod.out_channels
+    m = ops.mask_prep(mod.Feature_Mask)
+    Z = _empty(B, Cout, T, V, like=x0)
+    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(x0, 1, +1), PV(Z, 1, +1),
+               Cout, Cin, T, V, mask=m)
+    if training:
+        zst = ops.bn_finalize(ops.moments(Z, True), B, Cout * V, T, mod.bn, perm_V=V)
+    else:
+        zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
+    D0 = dst = None
+    if mod.has_down:
+        conv, bn = mod.down[0], mod.down[1]
+        D0 = _empty(B, Cout, T, V, like=x0)
+        ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
+        if training:
+            dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn)
+        else:
+            dst = ops.bn_eval_coef(bn, Cout)
+        H = ops.bn_apply(Z, zst, True, r=D0, rst=dst, relu=True)
+    else:
+        H = ops.bn_apply(Z, zst, True, r=x0, relu=True)
+    s = GcnSaved()
+    s.x0, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, Z, zst, D0, dst, H, m
+    return H, s
+
+
+def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None):
+    """Returns (dx0, {param_name: grad})."""
+    x0 = s.x0
+    B, Cin, T, V = x0.shape
+    Cout = mod.out_channels
+    g = {}
+    if mod.has_down:
+        conv, bnd = mod.down[0], mod.down[1]
+        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, r=s.D0, rst=s.dst)
+    else:
+        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True)
+    coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, Cout * V, B * T, s.zst,
+                                                               mod.bn, perm_V=V)
+    dZ = _empty(B, Cout, T, V, like=x0)
+    g_id = dD0 = None
+    if mod.has_down:
+        coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
+            rpart, B, Cout, B * T * V, s.dst, bnd)
+        dD0 = _empty(B, Cout, T, V, like=x0)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ)
+    else:
+        g_id = _empty(B, Cin, T, V, like=x0)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, dr=g_id, dx=dZ)
+    # einsum/bias grads: G(b,d,n) = dZ gathered back through shift_out (rotation +d)
+    dLW = torch.empty_like(mod.Linear_weight)
+    dLb = torch.empty_like(mod.Linear_bias)
+    ops.pw_dw(PV(dZ, 1, +1), PV(x0, 1, +1), dLW, Cout, Cin, T, V, mask=s.m, transpose=True,
+              dbias=dLb)
+    g["Linear_weight"], g["Linear_bias"] = dLW, dLb
+    dXt = _empty(B, Cin, T, V, like=x0)
+    ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ, 1, +1), PV(dXt), Cin, Cout, T, V)
+    dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=extra_dx)
+    g["Feature_Mask"] = ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V)
+    if mod.has_down:
+        dWd = torch.empty_like(conv.weight)
+        dbd = torch.empty_like(conv.bias)
+        ops.pw_dw(PV(dD0), PV(x0), dWd, Cout, Cin, T, V, dbias=dbd)
+        ops.pw_fwd(conv.weight, True, None, PV(dD0), PV(dx), Cin, Cout, T, V, accumulate=True)
+        g["down.0.weight"], g["down.0.bias"] = dWd, dbd
+    return dx, g
+
+
+# ======================================================================================
+# Shift_tcn
+# ======================================================================================
+class TcnSaved:
+    __slots__ = ("H", "ast", "As", "R", "S", "sst")
+
+
+def tcn_core_forward(mod, H, training):
+    """bn -> shift_in -> temporal_linear -> ReLU -> shift_out; returns (S, bn2 stats, saved)
+    where S is the shift_out output BEFORE bn2."""
+    B, C, T, V = H.shape
+    Cout = mod.out_channels
+    si, so = mod.shift_in, mod.shift_out
+    stride = so.stride
+    if training:
+        ast = ops.bn_finalize(ops.moments(H, False), B, C, T * V, mod.bn)
+    else:
+        ast = ops.bn_eval_coef(mod.bn, C)
+    As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=ast.scale,
+                        shift=ast.shift)
+    R = _empty(B, Cout, T, V, like=H)
+    tl = mod.temporal_linear
+    ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
+    To = T // stride
+    stats = _empty(B * Cout * 2, like=H) if training else None
+    S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
+    if training:
+        sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2)
+    else:
+        sst = ops.bn_eval_coef(mod.bn2, Cout)
+    s = TcnSaved()
+    s.H, s.ast, s.As, s.R, s.S, s.sst = H, ast, As, R, S, sst
+    return S, sst, s
+
+
+def tcn_core_backward(mod, s: TcnSaved, dS):
+    """dS: gradient w.r.t. S (pre-bn2). Returns (dH, grads)."""
+    H = s.H
+    B, C, T, V = H.shape
+    Cout = mod.out_channels
+    si, so = mod.shift_in, mod.shift_out
+    g = {}
+    dRp, g["shift_out.xpos"], g["shift_out.ypos"] = ops.tshift_bwd(
+        dS, s.R, so.xpos.detach(), so.ypos.detach(), so.stride, relu_mask=True)
+    tl = mod.temporal_linear
+    dWt = torch.empty_like(tl.weight)
+    dbt = torch.empty_like(tl.bias)
+    ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
+    g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
+    dAs = _empty(B, C, T, V, like=H)
+    ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
+    dA, g["shift_in.xpos"], g["shift_in.ypos"] = ops.tshift_bwd(
+        dAs, H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=s.ast.scale,
+        shift=s.ast.shift)
+    part, _ = ops.bn_bwd_reduce(dA, None, False, H, s.ast, False)
+    coef, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, C, B * T * V, s.ast,
+                                                             mod.bn)
+    dH = ops.bn_bwd_apply(dA, None, False, H, coef, False)
+    return dH, g
+
+
+# ======================================================================================
+# tcn (kernel_size = 1 residual conv + BN)
+# ======================================================================================
+class ConvBnSaved:
+    __slots__ = ("x", "Rc", "rst", "To")
+
+
+def convbn_core_forward(mod, x, training):
+    B, Cin, T, V = x.shape
+    conv, bn = mod.conv, mod.bn
+    Cout = conv.out_channels
+    s_t = mod.stride
+    To = (T - 1) // s_t + 1
+    Rc = _empty(B, Cout, To, V, like=x)
+    ops.pw_fwd(conv.weight, False, conv.bias, PV(x, s_t), PV(Rc), Cout, Cin, To, V)
+    if training:
+        rst = ops.bn_finalize(ops.moments(Rc, False), B, Cout, To * V, bn)
+    else:
+        rst = ops.bn_eval_coef(bn, Cout)
+    s = ConvBnSaved()
+    s.x, s.Rc, s.rst, s.To = x, Rc, rst, To
+    return Rc, rst, s
+
+
+def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate):
+    """Conv weight/bias grads and dx (+)= W^T dRc at the strided rows."""
+    B, Cin, T, V = s.x.shape
+    conv = mod.conv
+    Cout = conv.out_channels
+    dW = torch.empty_like(conv.weight)
+    db = torch.empty_like(conv.bias)
+    ops.pw_dw(PV(dRc), PV(s.x, mod.stride), dW, Cout, Cin, s.To, V, dbias=db)
+    ops.pw_fwd(conv.weight, True, None, PV(dRc), PV(dx, mod.stride), Cin, Cout, s.To, V,
+               accumulate=accumulate)
+    return {"conv.weight": dW, "conv.bias": db}
+
+
+# ======================================================================================
+# TCN_GCN_unit
+# ======================================================================================
+class UnitSaved:
+    __slots__ = ("x", "gs", "ts", "rs", "out")
+
+
+def unit_forward(unit, x, training):
+    H, gs = gcn_forward(unit.gcn1, x, training)
+    S, sst, ts = tcn_core_forward(unit.tcn1, H, training)
+    rs = None
+    if unit.residual_kind == "conv":
+        Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
+        out = ops.bn_apply(S, sst, False, r=Rc, rst=rst, relu=True)
+    elif unit.residual_kind == "identity":
+        out = ops.bn_apply(S, sst, False, r=x, relu=True)
+    else:
+        out = ops.bn_apply(S, sst, False, relu=True)
+    s = UnitSaved()
+    s.x, s.gs, s.ts, s.rs, s.out = x, gs, ts, rs, out
+    return out, s
+
+
+def unit_backward(unit, s: UnitSaved, dout):
+    ts = s.ts
+    S = ts.S
+    B, Cout, To, V = S.shape
+    kind = unit.residual_kind
+    g = {}
+    if kind == "conv":
+        part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False, r=s.rs.Rc,
+                                        rst=s.rs.rst)
+    else:
+        part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False)
+    coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
+        part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
+    dS = torch.empty_like(S)
+    dres = None
+    if kind == "conv":
+        coefR, g["residual.bn.weight"], g["residual.bn.bias"] = ops.bn_bwd_finalize(
+            rpart, B, Cout, B * To * V, s.rs.rst, unit.residual.bn)
+        dres = torch.empty_like(s.rs.Rc)
+        ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, r=s.rs.Rc, rcoef=coefR, dr=dres,
+                         dx=dS)
+    elif kind == "identity":
+        dres = torch.empty_like(s.x)
+        ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dr=dres, dx=dS)
+    else:
+        ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dx=dS)
+    dH, gt = tcn_core_backward(unit.tcn1, ts, dS)
+    g.update({"tcn1." + k: v for k, v in gt.items()})
+    dx, gg = gcn_backward(unit.gcn1, s.gs, dH, extra_dx=dres if kind == "identity" else None)
+    g.update({"gcn1." + k: v for k, v in gg.items()})
+    if kind == "conv":
+        gr = convbn_dx_and_dw(unit.residual, s.rs, dres, dx, accumulate=True)
+        g.update({"residual." + k: v for k, v in gr.items()})
+    return dx, g
+
+
+# ======================================================================================
+# autograd Functions (module forward -> Function.apply(module, input, *params))
+# ======================================================================================
+def trainable(module):
+    return [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+
+
+class _BlockFunction(torch.autograd.Function):
+    """Generic Function: ``fwd(module, x, training) -> (y, saved)`` and
+    ``bwd(module, saved, dy) -> (dx, {param_name: grad})``."""
+
+    @staticmethod
+    def forward(ctx, impl, module, x, *params):
+        fwd, bwd = impl
+        training = module.training
+        if not training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            pass  # eval-mode forward; backward below refuses (BN in eval has no batch stats)
+        y, saved = fwd(module, x.contiguous(), training)
+        ctx.impl, ctx.module, ctx.saved, ctx.training = impl, module, saved, training
+        ctx.names = [n for n, _ in trainable(module)]
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if not ctx.training:
+            raise NotImplementedError(
+                "backward through an eval-mode (running-stats) Shift-GCN block is not "
+                "supported by the HIP path; call .train() for training")
+        _, bwd = ctx.impl
+        dx, grads = bwd(ctx.module, ctx.saved, dy.contiguous())
+        ctx.saved = None
+        return (None, None, dx) + tuple(grads.get(n) for n in ctx.names)
+
+
+def run_block(impl, module, x):
+    params = [p for _, p in trainable(module)]
+    return _BlockFunction.apply(impl, module, x, *params)
+
+
+def _gcn_standalone_bwd(mod, s, dy):
+    return gcn_backward(mod, s, dy)
+
+
+def _tcn_standalone_fwd(mod, H, training):
+    S, sst, ts = tcn_core_forward(mod, H, training)
+    y = ops.bn_apply(S, sst, False)
+    return y, ts
+
+
+def _tcn_standalone_bwd(mod, ts, dy):
+    S = ts.S
+    B, C, To, V = S.shape
+    part, _ = ops.bn_bwd_reduce(dy, None, False, S, ts.sst, False)
+    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, ts.sst, mod.bn2)
+    dS = ops.bn_bwd_apply(dy, None, False, S, coef, False)
+    dH, g = tcn_core_backward(mod, ts, dS)
+    g["bn2.weight"], g["bn2.bias"] = dg, db
+    return dH, g
+
+
+def _convbn_standalone_fwd(mod, x, training):
+    Rc, rst, s = convbn_core_forward(mod, x, training)
+    return ops.bn_apply(Rc, rst, False), s
+
+
+def _convbn_standalone_bwd(mod, s, dy):
+    B, C, To, V = s.Rc.shape
+    part, _ = ops.bn_bwd_reduce(dy, None, False, s.Rc, s.rst, False)
+    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, s.rst, mod.bn)
+    dRc = ops.bn_bwd_apply(dy, None, False, s.Rc, coef, False)
+    dx = torch.zeros_like(s.x)
+    g = convbn_dx_and_dw(mod, s, dRc, dx, accumulate=True)
+    g["bn.weight"], g["bn.bias"] = dg, db
+    return dx, g
+
+
+GCN_IMPL = (gcn_forward, _gcn_standalone_bwd)
+TCN_IMPL = (_tcn_standalone_fwd, _tcn_standalone_bwd)
+CONVBN_IMPL = (_convbn_standalone_fwd, _convbn_standalone_bwd)
+UNIT_IMPL = (unit_forward, unit_backward)

@@ -80,3 +80,179 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
                              _ptr(ws), nbytes, B, C, H, W, stride, _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd")
     return gin, gx, gy
+
+
+# --------------------------------------------------------------------------------------
+# pointwise (1x1) contraction with fused joint-shift gathers
+# --------------------------------------------------------------------------------------
+class PlaneView:
+    """Plane-operand addressing of include/shiftgcn.h: element (b, ch, n = t*V + v) at
+    ``t.data[b*bstride + ch*cstride + (t*tstride)*V + (v + rsign*ch) mod V]``."""
+
+    __slots__ = ("t", "bstride", "cstride", "tstride", "rsign")
+
+    def __init__(self, t, tstride=1, rsign=0):
+        check_input(t, "plane operand")
+        self.t = t
+        self.bstride = t.stride(0)
+        self.cstride = t.stride(1)
+        self.tstride = tstride
+        self.rsign = rsign
+
+
+def pw_fwd(w, w_mcontig, bias, x: PlaneView, out: PlaneView, M, K, T, V, mask=None,
+           relu=False, accumulate=False):
+    check_input(w, "weight")
+    _opt(bias, "bias"), _opt(mask, "mask")
+    B = x.t.shape[0]
+    lib = _lib.load()
+    rc = lib.sgcn_pw_fwd(_ptr(w), int(w_mcontig), _ptr(bias), _ptr(x.t), x.bstride, x.cstride,
+                         x.tstride, x.rsign, _ptr(mask), _ptr(out.t), out.bstride, out.cstride,
+                         out.tstride, out.rsign, int(relu), int(accumulate), B, M, K, T, V,
+                         _stream(x.t))
+    _lib.check(rc, "sgcn_pw_fwd")
+    return out.t
+
+
+def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=False,
+          accumulate=False, dbias=None, dbias_accumulate=False):
+    check_input(dw, "dw")
+    _opt(dbias, "dbias"), _opt(mask, "mask")
+    B = g.t.shape[0]
+    lib = _lib.load()
+    nbytes = lib.sgcn_pw_dw_ws_bytes(B, M, Nc, T, V)
+    ws = torch.empty((nbytes + 3) // 4, device=g.t.device, dtype=_F32)
+    rc = lib.sgcn_pw_dw(_ptr(g.t), g.bstride, g.cstride, g.tstride, g.rsign, _ptr(x.t),
+                        x.bstride, x.cstride, x.tstride, x.rsign, _ptr(mask), _ptr(dw),
+                        int(transpose), int(accumulate), _ptr(dbias), int(dbias_accumulate),
+                        _ptr(ws), nbytes, B, M, Nc, T, V, _stream(g.t))
+    _lib.check(rc, "sgcn_pw_dw")
+    return dw
+
+
+# --------------------------------------------------------------------------------------
+# BatchNorm / unit tails
+# --------------------------------------------------------------------------------------
+def moments(x, per_joint):
+    check_input(x, "input")
+    B, C, T, V = x.shape
+    part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=x.device, dtype=_F32)
+    rc = _lib.load().sgcn_moments(_ptr(x), _ptr(part), B, C, T, V, int(per_joint), _stream(x))
+    _lib.check(rc, "sgcn_moments")
+    return part
+
+
+class BnStats:
+    """Batch statistics and apply coefficients of one BatchNorm call (local feature order)."""
+
+    __slots__ = ("mean", "invstd", "scale", "shift")
+
+    def __init__(self, F, device):
+        buf = torch.empty((4, F), device=device, dtype=_F32)
+        self.mean, self.invstd, self.scale, self.shift = buf[0], buf[1], buf[2], buf[3]
+
+
+def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
+    """Training-mode statistics of ``bn`` (an nn.BatchNorm*d) from partials; updates its
+    running stats / num_batches_tracked exactly once, like ``bn.forward`` in train()."""
+    st = BnStats(F, part.device)
+    lib = _lib.load()
+    track = training and bn.track_running_stats and bn.running_mean is not None
+    momentum = bn.momentum if bn.momentum is not None else 0.0
+    rc = lib.sgcn_bn_finalize(
+        _ptr(part), B, F, n_part, perm_V, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps),
+        float(momentum), _ptr(bn.running_mean) if track else None,
+        _ptr(bn.running_var) if track else None,
+        _ptr(bn.num_batches_tracked) if track else None, _ptr(st.mean), _ptr(st.invstd),
+        _ptr(st.scale), _ptr(st.shift), _stream(part))
+    _lib.check(rc, "sgcn_bn_finalize")
+    return st
+
+
+def bn_eval_coef(bn, F, perm_V=0, device=None):
+    st = BnStats(F, bn.running_mean.device)
+    rc = _lib.load().sgcn_bn_eval_coef(F, perm_V, _ptr(bn.weight), _ptr(bn.bias),
+                                       _ptr(bn.running_mean), _ptr(bn.running_var),
+                                       float(bn.eps), _ptr(st.scale), _ptr(st.shift),
+                                       _stream(bn.running_mean))
+    _lib.check(rc, "sgcn_bn_eval_coef")
+    return st
+
+
+def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False, out=None):
+    check_input(x, "input")
+    if r is not None:
+        check_input(r, "residual")
+    B, C, T, V = x.shape
+    y = torch.empty_like(x) if out is None else out
+    rc = _lib.load().sgcn_bn_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift), int(per_joint),
+                                   _ptr(r), _ptr(rst.scale) if rst else None,
+                                   _ptr(rst.shift) if rst else None, int(relu), _ptr(y), B, C,
+                                   T, V, _stream(x))
+    _lib.check(rc, "sgcn_bn_apply")
+    return y
+
+
+def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats = None):
+    check_input(dy, "grad_output")
+    B, C, T, V = x.shape
+    dev = x.device
+    part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=dev, dtype=_F32)
+    rpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if r is not None else None
+    rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(st.mean),
+                                        _ptr(st.invstd), int(per_joint), _ptr(r),
+                                        _ptr(rst.mean) if rst else None,
+                                        _ptr(rst.invstd) if rst else None, _ptr(part),
+                                        _ptr(rpart), B, C, T, V, _stream(x))
+    _lib.check(rc, "sgcn_bn_bwd_reduce")
+    return part, rpart
+
+
+def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
+    """Returns (coef[3,F], dgamma, dbeta) with dgamma/dbeta in the module's layout."""
+    dev = part.device
+    coef = torch.empty((3, F), device=dev, dtype=_F32)
+    dgamma = torch.empty_like(bn.weight) if bn.weight is not None else None
+    dbeta = torch.empty_like(bn.bias) if bn.bias is not None else None
+    rc = _lib.load().sgcn_bn_bwd_finalize(_ptr(part), B, F, int(n_total), perm_V,
+                                          _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
+                                          _ptr(dgamma), _ptr(dbeta), 0, _ptr(coef),
+                                          _stream(part))
+    _lib.check(rc, "sgcn_bn_bwd_finalize")
+    return coef, dgamma, dbeta
+
+
+def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, dx=None):
+    B, C, T, V = x.shape
+    dx = torch.empty_like(x) if dx is None else dx
+    rc = _lib.load().sgcn_bn_bwd_apply(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(coef),
+                                       int(per_joint), _ptr(r), _ptr(rcoef), _ptr(dx),
+                                       _ptr(dr), B, C, T, V, _stream(x))
+    _lib.check(rc, "sgcn_bn_bwd_apply")
+    return dx
+
+
+def mask_prep(mask):
+    check_input(mask, "Feature_Mask")
+    m = torch.empty_like(mask)
+    rc = _lib.load().sgcn_mask_prep(_ptr(mask), _ptr(m), mask.numel(), _stream(mask))
+    _lib.check(rc, "sgcn_mask_prep")
+    return m
+
+
+def gcn_dx_finish(dxt, x0, m, add1=None, add2=None):
+    B, C, T, V = dxt.shape
+    dx = torch.empty_like(dxt)
+    part = torch.empty((B * C * V,), device=dxt.device, dtype=_F32)
+    rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1), _ptr(add2),
+                                        _ptr(dx), _ptr(part), B, C, T, V, _stream(dxt))
+    _lib.check(rc, "sgcn_gcn_dx_finish")
+    return dx, part
+
+
+def mask_grad_finalize(part, mask, B, C, V):
+    dmask = torch.empty_like(mask)
+    rc = _lib.load().sgcn_mask_grad_finalize(_ptr(part), _ptr(mask), B, C, V, _ptr(dmask), 0,
+                                             _stream(mask))
+    _lib.check(rc, "sgcn_mask_grad_finalize")
+    return dmask

@@ -1,0 +1,182 @@
+"""GPU parity of the fused HIP blocks against the CPU oracle (itself pinned to the
+reference modules) and the committed golden fixtures.
+
+Tolerance (fp32, north_star: 1e-5): outputs and input gradients within 2e-5 relative to
+the tensor's max magnitude; parameter gradients (long reductions) within 1e-4 relative;
+shift-position gradients (sign-normalised, +-0.01) bit-exact except where the reduced
+position gradient is within float rounding of zero (<= 1 channel allowed).
+"""
+import numpy as np
+import pytest
+import torch
+
+import formula
+from gen_fixtures import (BLOCK_CASES, MODEL_CASES, block_case_inputs, build_block,
+                          model_case_inputs)
+from oracle import model_oracle as mo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel_close(a, b, tol, what=""):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    scale = max(float(np.abs(b).max()) if b.size else 0.0, 1e-6)
+    err = float(np.abs(a - b).max()) if a.size else 0.0
+    assert err <= tol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _shift_grads_close(a, b, what):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert (a != b).sum() <= 1, f"{what}: {(a != b).sum()} position-grad mismatches"
+
+
+def _pair(kind, cin, cout, V, stride, seed):
+    import shiftgcn
+    ref = build_block(mo, kind, cin, cout, V, stride)
+    formula.fill_state(ref, seed=seed)
+    ours = build_block(shiftgcn, kind, cin, cout, V, stride).to(DEV)
+    ours.load_state_dict(ref.state_dict())
+    ref.train()
+    ours.train()
+    return ref, ours
+
+
+def _run_pair(ref, ours, x, g):
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(g)
+    xo = x.to(DEV).requires_grad_(True)
+    yo = ours(xo)
+    yo.backward(g.to(DEV))
+    torch.cuda.synchronize()
+    return xr, yr, xo, yo
+
+
+def _compare(ref, ours, xr, yr, xo, yo, tag):
+    _rel_close(yo.detach().cpu(), yr.detach(), 2e-5, f"{tag} out")
+    _rel_close(xo.grad.cpu(), xr.grad, 2e-5, f"{tag} dx")
+    po = dict(ours.named_parameters())
+    for n, p in ref.named_parameters():
+        if p.grad is None:
+            assert po[n].grad is None, n
+            continue
+        go = po[n].grad.cpu()
+        if n.endswith(("xpos", "ypos")):
+            _shift_grads_close(go.numpy(), p.grad.numpy(), f"{tag} {n}")
+        else:
+            _rel_close(go, p.grad, 1e-4, f"{tag} grad {n}")
+    bo = dict(ours.named_buffers())
+    for n, b in ref.named_buffers():
+        if b.dtype.is_floating_point:
+            _rel_close(bo[n].cpu(), b, 2e-5, f"{tag} buffer {n}")
+        else:
+            assert int(bo[n]) == int(b), n
+
+
+@pytest.mark.parametrize("case", BLOCK_CASES, ids=[c[0] for c in BLOCK_CASES])
+def test_block_matches_golden_fixture(golden, case):
+    """Same deterministic weights/inputs the reference modules ran on."""
+    import shiftgcn
+    fx = golden("block_fixtures.npz")
+    name, kind, cin, cout, NM, T, V, stride = case
+    m = build_block(shiftgcn, kind, cin, cout, V, stride)
+    formula.fill_state(m, seed=31 + sum(map(ord, name)))
+    m = m.to(DEV).train()
+    x, g = block_case_inputs(*case)
+    xo = x.to(DEV).requires_grad_(True)
+    y = m(xo)
+    y.backward(g.to(DEV))
+    _rel_close(y.detach().cpu(), fx[f"blk_{name}_out"], 2e-5, "out")
+    _rel_close(xo.grad.cpu(), fx[f"blk_{name}_gx"], 2e-5, "dx")
+    for pn, p in m.named_parameters():
+        key = f"blk_{name}_grad.{pn}"
+        if p.grad is None:
+            continue
+        if pn.endswith(("xpos", "ypos")):
+            _shift_grads_close(p.grad.cpu().numpy(), fx[key], pn)
+        else:
+            _rel_close(p.grad.cpu(), fx[key], 1e-4, pn)
+    for bn, b in m.named_buffers():
+        if b.dtype.is_floating_point:
+            _rel_close(b.cpu(), fx[f"blk_{name}_buf.{bn}"], 2e-5, bn)
+
+
+REAL_CASES = [
+    # (kind, cin, cout, NM, T, V, stride) at the model's real channel widths
+    ("gcn", 3, 64, 4, 20, 25, 1),
+    ("gcn", 64, 64, 4, 20, 25, 1),
+    ("gcn", 64, 128, 3, 12, 25, 1),
+    ("gcn", 128, 256, 2, 10, 33, 1),
+    ("tcn", 64, 64, 4, 20, 25, 1),
+    ("tcn", 128, 128, 3, 16, 25, 2),
+    ("unit", 64, 128, 3, 20, 25, 2),
+    ("unit", 128, 128, 3, 12, 25, 1),
+    ("unit", 128, 256, 2, 16, 33, 2),
+    ("unit_nores", 3, 64, 4, 20, 25, 1),
+]
+
+
+@pytest.mark.parametrize("case", REAL_CASES, ids=["-".join(map(str, c)) for c in REAL_CASES])
+def test_block_matches_oracle_real_widths(case):
+    kind, cin, cout, NM, T, V, stride = case
+    ref, ours = _pair(kind, cin, cout, V, stride, seed=cin * 31 + cout + T)
+    x = formula.tensor((NM, cin, T, V), 5 + cin + cout, 1.0)
+    To = T // stride if kind != "gcn" else T
+    g = formula.tensor((NM, cout, To, V), 7 + cin + cout, 1.0)
+    xr, yr, xo, yo = _run_pair(ref, ours, x, g)
+    _compare(ref, ours, xr, yr, xo, yo, "-".join(map(str, case)))
+
+
+def test_standalone_tcn_residual_conv_matches_oracle():
+    import shiftgcn
+    ref = mo.tcn(64, 128, kernel_size=1, stride=2)
+    formula.fill_state(ref, seed=5)
+    ours = shiftgcn.tcn(64, 128, kernel_size=1, stride=2).to(DEV)
+    ours.load_state_dict(ref.state_dict())
+    x = formula.tensor((3, 64, 21, 25), 9, 1.0)
+    g = formula.tensor((3, 128, 11, 25), 10, 1.0)
+    xr, yr, xo, yo = _run_pair(ref.train(), ours.train(), x, g)
+    _compare(ref, ours, xr, yr, xo, yo, "tcn")
+
+
+def test_eval_mode_forward_matches_oracle():
+    ref, ours = _pair("unit", 64, 128, 25, 2, seed=77)
+    ref.eval()
+    ours.eval()
+    x = formula.tensor((2, 64, 20, 25), 3, 1.0)
+    with torch.no_grad():
+        _rel_close(ours(x.to(DEV)).cpu(), ref(x), 2e-5, "eval unit")
+
+
+@pytest.mark.parametrize("case", MODEL_CASES, ids=[c[0] for c in MODEL_CASES])
+def test_model_matches_golden_fixture(golden, case):
+    """Full Model at bs=2, T=300 (NTU: (2,3,300,25,2); MediaPipe: (2,3,300,33,1))."""
+    import shiftgcn
+    fx = golden("model_fixtures.npz")
+    name, num_class, V, M, N, T = case
+    m = shiftgcn.Model(num_class=num_class, num_point=V, num_person=M,
+                       graph="graph.ntu_rgb_d.Graph")
+    formula.fill_state(m, seed=97 + sum(map(ord, name)))
+    m = m.to(DEV)
+    x, labels = model_case_inputs(*case)
+    m.eval()
+    with torch.no_grad():
+        _rel_close(m(x.to(DEV)).cpu(), fx[f"model_{name}_logits_eval"], 1e-4, "eval logits")
+    m.train()
+    logits = m(x.to(DEV))
+    loss = torch.nn.functional.cross_entropy(logits, labels.to(DEV))
+    loss.backward()
+    _rel_close(logits.detach().cpu(), fx[f"model_{name}_logits_train"], 1e-4, "train logits")
+    assert abs(float(loss) - float(fx[f"model_{name}_loss"])) < 1e-4 * max(1, float(loss))
+    names = list(fx[f"model_{name}_grad_names"])
+    params = dict(m.named_parameters())
+    gnorm = np.array([float(params[n].grad.double().norm()) for n in names])
+    np.testing.assert_allclose(gnorm, fx[f"model_{name}_grad_norm"], rtol=2e-3, atol=1e-7)
+    mism = 0
+    for n in names:
+        if n.endswith(("xpos", "ypos")):
+            mism += int((params[n].grad.cpu().numpy() != fx[f"model_{name}_grad.{n}"]).sum())
+    assert mism <= 2, f"{mism} shift-position grad mismatches"
