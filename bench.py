@@ -1,0 +1,242 @@
+"""Shift-GCN training throughput on MI355X: skeleton clips/s, fwd+bwd (+SGD step).
+
+BASELINE.json metric: "skeleton clips/sec fwd+bwd, NTU (3,300,25,2) bs=64; 1/2/4/8 MI355X".
+One step = one reference training iteration (main.py:397-416) on one synthetic NTU batch
+per GPU: Model forward (10 fused TCN_GCN_units on the HIP path), CrossEntropy, backward,
+[RCCL gradient all-reduce for N>1], SGD(momentum 0.9, nesterov, per-param weight decay).
+Inputs are resident in HBM before the timed region. Weak scaling: 64 clips per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ntu|mp] [--graph 0|1]
+N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (value = whole-job clips/s), with:
+  roofline     — dominant kernel class of the timed region, achieved algorithmic
+                 FLOP/s (or bytes/s) from HIP events around every launch of it;
+  cpu_baseline — the PyTorch-eager CPU restatement (oracle/, "port") on the host cores,
+                 on a bounded sample (2 clips, fwd+bwd+SGD), rank 0 / N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(REPO, "shift-gcn_amd"), REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # name: (num_class, V, M, T, graph)
+    "ntu": (60, 25, 2, 300, "graph.ntu_rgb_d.Graph"),
+    "mp": (2, 33, 1, 300, "graph.mediapipe_pose.Graph"),
+}
+# algorithmic fwd+bwd GFLOP per clip (torch FlopCounter on the reference model)
+GFLOP_PER_CLIP = {"ntu": 21.416, "mp": 14.134}
+PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 matrix (= vector) dense peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0      # HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="clips per GPU")
+    ap.add_argument("--config", default="ntu", choices=sorted(CONFIGS))
+    ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--roofline", type=int, default=1)
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, seconds_budget=30.0):
+    """The oracle (PyTorch-eager CPU restatement of the reference model) on a bounded
+    sample: 2 clips of the same workload, one fwd+bwd+SGD iteration per sample."""
+    from oracle import model_oracle as mo
+    num_class, V, M, T, _ = CONFIGS[cfg]
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch.manual_seed(1)
+        model = mo.Model(num_class=num_class, num_point=V, num_person=M, graph="unused").train()
+        opt = torch.optim.SGD(mo.sgd_param_groups(model, 0.1), lr=0.1, momentum=0.9,
+                              nesterov=True)
+        g = torch.Generator().manual_seed(0)
+        n = 2
+        x = torch.randn(n, 3, T, V, M, generator=g)
+        y = torch.randint(0, num_class, (n,), generator=g)
+
+        def it():
+            loss = torch.nn.functional.cross_entropy(model(x), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+
+        it()  # warm-up
+        times = []
+        t_all = time.perf_counter()
+        while len(times) < 3 and time.perf_counter() - t_all < seconds_budget:
+            t0 = time.perf_counter()
+            it()
+            times.append(time.perf_counter() - t0)
+        times.sort()
+        med = times[len(times) // 2]
+        model_name = ""
+        try:
+            with open("/proc/cpuinfo") as f:
+                for line in f:
+                    if line.startswith("model name"):
+                        model_name = line.split(":", 1)[1].strip()
+                        break
+        except OSError:
+            pass
+        return {"value": round(n / med, 4), "unit": "clips/s", "cores": threads,
+                "kind": "port",
+                "sample": f"{cfg.upper()} bs={n} (2 clips of the bs=64 workload), fwd+bwd+SGD, "
+                          f"median of {len(times)} after 1 warm-up, {med:.2f} s/iter; "
+                          f"{model_name}"}
+    finally:
+        torch.set_num_threads(prev)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import shiftgcn
+    from shiftgcn import ops, train
+    from shiftgcn.dist import GradAllReduce, broadcast_parameters
+
+    num_class, V, M, T, graph = CONFIGS[args.config]
+    torch.manual_seed(1)                                # main.py:24-27 init seed
+    model = shiftgcn.Model(num_class=num_class, num_point=V, num_person=M, graph=graph)
+    model = model.to(dev).train()
+    if distributed:
+        broadcast_parameters(model)
+    opt = train.build_optimizer(model, base_lr=0.1)
+    sync = GradAllReduce(model) if distributed else None
+    gen = torch.Generator().manual_seed(1000 + rank)
+    x = torch.randn(args.batch, 3, T, V, M, generator=gen).to(dev)
+    label = torch.randint(0, num_class, (args.batch,), generator=gen).to(dev)
+
+    def step():
+        return train.train_step(model, opt, x, label, grad_sync=sync)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    runner = step
+    if args.graph:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(g):
+            step()
+        runner = g.replay
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    clips = args.batch * world * args.steps
+    value = clips / elapsed
+    ms = 1000.0 * elapsed / args.steps
+
+    roof = None
+    if args.roofline and rank == 0:
+        # HIP events around every launch of each kernel class, over K eager steps
+        timer = ops.LaunchTimer()
+        ops.set_launch_timer(timer)
+        torch.cuda.synchronize()
+        for _ in range(max(1, min(args.steps, 5))):
+            step()
+        torch.cuda.synchronize()
+        ops.set_launch_timer(None)
+        summ = timer.summary()
+        dom = max(summ, key=lambda k: summ[k]["ms_total"])
+        d = summ[dom]
+        mfma = d["flops"] > 0
+        per_launch_s = d["ms_total"] / d["launches"] / 1e3
+        if mfma:
+            achieved = d["flops"] / d["launches"] / per_launch_s / 1e12
+            peak, unit = PEAK_FP32_TFLOPS, "TFLOP/s"
+        else:
+            achieved = d["bytes"] / d["launches"] / per_launch_s / 1e9
+            peak, unit = PEAK_HBM_GBS, "GB/s"
+        roof = {"bound": "mfma" if mfma else "hbm", "kernel": dom,
+                "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "launches_per_step": d["launches"] // max(1, min(args.steps, 5)),
+                "avg_launch_us": round(per_launch_s * 1e6, 2),
+                "step_breakdown_ms": {k: round(v["ms_total"] / max(1, min(args.steps, 5)), 3)
+                                      for k, v in sorted(summ.items())},
+                "whole_step_frac_of_fp32_peak": round(
+                    value / world * GFLOP_PER_CLIP[args.config] / 1e3 / PEAK_FP32_TFLOPS, 4)}
+
+    cpu = None
+    if args.cpu_baseline and rank == 0 and world == 1:
+        cpu = cpu_baseline(args.config)
+
+    if rank == 0:
+        line = {
+            "metric": "skeleton clips/sec fwd+bwd, NTU (3,300,25,2) bs=64; 1/2/4/8 MI355X"
+            if args.config == "ntu" else
+            "skeleton clips/sec fwd+bwd, MediaPipe (3,300,33,1) bs=64",
+            "value": round(value, 2),
+            "unit": "clips/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic N(0,1) clips, random-init weights (seeded)",
+            "config": {"workload": f"{args.config.upper()} Shift-GCN training step "
+                                   f"(fwd+CE+bwd+SGD), x=({args.batch},3,{T},{V},{M}) per GPU",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "parallelism": f"dp{world}", "hipgraph": bool(args.graph)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

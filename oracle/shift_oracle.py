@@ -35,12 +35,11 @@ from __future__ import annotations
 import numpy as np
 
 F32 = np.float32
-ONE = F32(1.0)
 
 
 def _floor_int(v: np.ndarray) -> np.ndarray:
-    """``int x1 = floorf(x)`` (.cu:49) on a float32 vector."""
-    return np.floor(v.astype(F32)).astype(np.int64)
+    """``int x1 = floorf(x)`` (.cu:49) on a float vector."""
+    return np.floor(v).astype(np.int64)
 
 
 def _taps(plane: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.ndarray:
@@ -51,41 +50,44 @@ def _taps(plane: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.ndarray:
     B, C, H, W = plane.shape
     hh_b, ww_b = np.broadcast_arrays(hh, ww)
     valid = (hh_b >= 0) & (ww_b >= 0) & (hh_b < H) & (ww_b < W)
+    if H == 0 or W == 0:
+        return np.zeros((B, C) + hh_b.shape[1:], plane.dtype)
     hc = np.clip(hh_b, 0, H - 1)
     wc = np.clip(ww_b, 0, W - 1)
     cidx = np.arange(C)[:, None, None]
     out = plane[:, cidx, hc, wc]
-    return np.where(valid[None], out, F32(0)).astype(F32)
+    return np.where(valid[None], out, plane.dtype.type(0)).astype(plane.dtype)
 
 
 def _bilinear(q11, q21, q12, q22, dx, dy):
     """``q11*(1-dx)*(1-dy) + q21*dx*(1-dy) + q12*(1-dx)*dy + q22*dx*dy`` (.cu:73),
     evaluated left to right in float32 (each product/sum rounded once)."""
-    omdx = ONE - dx
-    omdy = ONE - dy
+    one = q11.dtype.type(1)
+    omdx = one - dx
+    omdy = one - dy
     t1 = (q11 * omdx) * omdy
     t2 = (q21 * dx) * omdy
     t3 = (q12 * omdx) * dy
     t4 = (q22 * dx) * dy
-    return (((t1 + t2) + t3) + t4).astype(F32)
+    return (((t1 + t2) + t3) + t4).astype(q11.dtype)
 
 
 def _frac(pos: np.ndarray):
     """Per-channel integer/fractional split: ``x1=floorf(x); dx=x-x1`` (.cu:49-71)."""
-    pos = pos.astype(F32)
     i1 = _floor_int(pos)
-    d = (pos - i1.astype(F32)).astype(F32)
+    d = (pos - i1.astype(pos.dtype)).astype(pos.dtype)
     return i1, d
 
 
 def shift_forward(inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray, stride: int) -> np.ndarray:
     """Forward temporal shift. ``ypos`` must already carry the +0.5 for stride != 1
     (``shift.py:17-18``). Output shape (B, C, H // stride, W) (.cu:408)."""
-    inp = np.ascontiguousarray(inp, dtype=F32)
+    inp = np.ascontiguousarray(inp)
+    dt = inp.dtype
     B, C, H, W = inp.shape
     Ho = H // stride
-    x1, dx = _frac(xpos)
-    y1, dy = _frac(ypos)
+    x1, dx = _frac(xpos.astype(dt))
+    y1, dy = _frac(ypos.astype(dt))
     h = np.arange(Ho)[None, :, None] * stride                # h_offset = h*stride
     w = np.arange(W)[None, None, :]                          # w_offset = w
     hy1 = h + y1[:, None, None]
@@ -107,6 +109,8 @@ def _taps_stride2_top(gout: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.nd
     (C++ quotient, truncated) is bounds-checked against the top grid."""
     B, C, Ht, Wt = gout.shape
     hh_b, ww_b = np.broadcast_arrays(hh, ww)
+    if Ht == 0 or Wt == 0:
+        return np.zeros((B, C) + hh_b.shape[1:], gout.dtype)
     even = np.fmod(hh_b, 2) == 0
     hq = np.trunc(hh_b / 2).astype(np.int64)
     valid = even & (hq >= 0) & (ww_b >= 0) & (hq < Ht) & (ww_b < Wt)
@@ -114,17 +118,18 @@ def _taps_stride2_top(gout: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.nd
     wc = np.clip(ww_b, 0, Wt - 1)
     cidx = np.arange(C)[:, None, None]
     out = gout[:, cidx, hc, wc]
-    return np.where(valid[None], out, F32(0)).astype(F32)
+    return np.where(valid[None], out, gout.dtype.type(0)).astype(gout.dtype)
 
 
 def shift_bottom_backward(gout: np.ndarray, xpos: np.ndarray, ypos: np.ndarray,
                           H: int, stride: int) -> np.ndarray:
     """Input gradient: bilinear sample of ``grad_output`` at the reversed position
     ``(-xpos, -ypos)`` over the bottom grid (.cu:78-152 stride 1, .cu:155-256 stride 2)."""
-    gout = np.ascontiguousarray(gout, dtype=F32)
+    gout = np.ascontiguousarray(gout)
+    dt = gout.dtype
     B, C, Ht, W = gout.shape
-    x1, dx = _frac(-xpos.astype(F32))
-    y1, dy = _frac(-ypos.astype(F32))
+    x1, dx = _frac(-xpos.astype(dt))
+    y1, dy = _frac(-ypos.astype(dt))
     h = np.arange(H)[None, :, None]
     w = np.arange(W)[None, None, :]
     hy1 = h + y1[:, None, None]
@@ -149,12 +154,14 @@ def shift_position_backward(inp: np.ndarray, gout: np.ndarray, xpos: np.ndarray,
     """Per-output-element position gradients ``val_x*g`` and ``val_y*g`` (.cu:277-363).
 
     Returns the two (B, C, Ho, W) temporaries the reference materialises (.cu:480-481)."""
-    inp = np.ascontiguousarray(inp, dtype=F32)
-    gout = np.ascontiguousarray(gout, dtype=F32)
+    inp = np.ascontiguousarray(inp)
+    gout = np.ascontiguousarray(gout, dtype=inp.dtype)
+    dt = inp.dtype
+    one = dt.type(1)
     B, C, H, W = inp.shape
     Ho = H // stride
-    ix1, dx = _frac(xpos)
-    iy1, dy = _frac(ypos)
+    ix1, dx = _frac(xpos.astype(dt))
+    iy1, dy = _frac(ypos.astype(dt))
     h = np.arange(Ho)[None, :, None] * stride
     w = np.arange(W)[None, None, :]
     h1 = h + iy1[:, None, None]
@@ -168,9 +175,9 @@ def shift_position_backward(inp: np.ndarray, gout: np.ndarray, xpos: np.ndarray,
     dxb = dx[None, :, None, None]
     dyb = dy[None, :, None, None]
     # val_x = (1-dy)*(q21-q11)+dy*(q22-q12); val_y = (1-dx)*(q12-q11)+dx*(q22-q21)  (.cu:343-344)
-    val_x = ((ONE - dyb) * (q21 - q11) + dyb * (q22 - q12)).astype(F32)
-    val_y = ((ONE - dxb) * (q12 - q11) + dxb * (q22 - q21)).astype(F32)
-    return (val_x * gout).astype(F32), (val_y * gout).astype(F32)
+    val_x = ((one - dyb) * (q21 - q11) + dyb * (q22 - q12)).astype(dt)
+    val_y = ((one - dxb) * (q12 - q11) + dxb * (q22 - q21)).astype(dt)
+    return (val_x * gout).astype(dt), (val_y * gout).astype(dt)
 
 
 def reduce_position_grad(g_bchw: np.ndarray) -> np.ndarray:
@@ -180,24 +187,25 @@ def reduce_position_grad(g_bchw: np.ndarray) -> np.ndarray:
     ATen/CUDA; only the sign (and zero-ness) of the result is observable after
     :func:`apply_shift_constraint`. float64 accumulation keeps the sign robust."""
     g = g_bchw.astype(np.float64)
-    return g.mean(axis=0).sum(axis=2).sum(axis=1).astype(F32)
+    return g.mean(axis=0).sum(axis=2).sum(axis=1).astype(g_bchw.dtype)
 
 
 def apply_shift_constraint(gx: np.ndarray, gy: np.ndarray):
     """``applyShiftConstraint`` (.cu:370-395), including its float/double promotions:
     ``dr = sqrt(dy*dy)`` in float; ``dx/dr*0.0`` and ``dy/dr*0.01`` are float
     quotients times *double* literals, rounded to float on store; the ``dr == 0``
-    branch stores ``0.0`` and ``0.0001`` (as float)."""
-    gx = gx.astype(F32)
-    gy = gy.astype(F32)
-    dr = np.sqrt((gy * gy).astype(F32)).astype(F32)
+    branch stores ``0.0`` and ``0.0001`` (as float). (float64 inputs stay float64.)"""
+    dt = np.float64 if gy.dtype == np.float64 else F32
+    gx = gx.astype(dt)
+    gy = gy.astype(dt)
+    dr = np.sqrt((gy * gy).astype(dt)).astype(dt)
     nz = dr != 0
-    with np.errstate(divide="ignore", invalid="ignore"):
-        qx = (gx / np.where(nz, dr, ONE)).astype(F32)
-        qy = (gy / np.where(nz, dr, ONE)).astype(F32)
-    out_x = np.where(nz, (qx.astype(np.float64) * 0.0).astype(F32), F32(0.0))
-    out_y = np.where(nz, (qy.astype(np.float64) * 0.01).astype(F32), F32(0.0001))
-    return out_x.astype(F32), out_y.astype(F32)
+    safe = np.where(nz, dr, dt(1))
+    qx = (gx / safe).astype(dt)
+    qy = (gy / safe).astype(dt)
+    out_x = np.where(nz, (qx.astype(np.float64) * 0.0).astype(dt), dt(0.0))
+    out_y = np.where(nz, (qy.astype(np.float64) * 0.01).astype(dt), dt(0.0001))
+    return out_x.astype(dt), out_y.astype(dt)
 
 
 def shift_backward(gout: np.ndarray, inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray,
@@ -214,5 +222,4 @@ def shift_backward(gout: np.ndarray, inp: np.ndarray, xpos: np.ndarray, ypos: np
 def effective_ypos(ypos: np.ndarray, stride: int) -> np.ndarray:
     """``ShiftFunction.forward``'s ``ypos = ypos + 0.5`` for stride != 1 (``shift.py:14-18``),
     a float32 add."""
-    ypos = ypos.astype(F32)
-    return ypos if stride == 1 else (ypos + F32(0.5)).astype(F32)
+    return ypos if stride == 1 else (ypos + ypos.dtype.type(0.5)).astype(ypos.dtype)

@@ -18,6 +18,66 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+# --------------------------------------------------------------------------------------
+# optional launch timing (bench.py roofline): HIP events around each C-ABI call
+# --------------------------------------------------------------------------------------
+class LaunchTimer:
+    """Records (op, algorithmic flops, algorithmic bytes, start, end) for every C-ABI call
+    made while active, with events on the stream the kernels are launched on."""
+
+    def __init__(self, ops_filter=None):
+        self.ops_filter = ops_filter
+        self.records = []
+
+    def begin(self, op, flops, nbytes, device):
+        if self.ops_filter is not None and op not in self.ops_filter:
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream(device))
+        return (op, flops, nbytes, e0, e1, device)
+
+    def end(self, rec):
+        if rec is None:
+            return
+        rec[4].record(torch.cuda.current_stream(rec[5]))
+        self.records.append(rec[:5])
+
+    def summary(self):
+        """{op: {launches, ms_total, flops, bytes}} (call after a device sync)."""
+        out = {}
+        for op, fl, nb, e0, e1 in self.records:
+            d = out.setdefault(op, {"launches": 0, "ms_total": 0.0, "flops": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["ms_total"] += e0.elapsed_time(e1)
+            d["flops"] += fl
+            d["bytes"] += nb
+        return out
+
+
+_TIMER = None
+
+
+def set_launch_timer(timer):
+    global _TIMER
+    _TIMER = timer
+
+
+class _timed:
+    __slots__ = ("rec",)
+
+    def __init__(self, op, flops, nbytes, t):
+        self.rec = _TIMER.begin(op, flops, nbytes, t.device) if _TIMER is not None else None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        if self.rec is not None:
+            _TIMER.end(self.rec)
+        return False
+
+
 def _stream(t: torch.Tensor):
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -54,8 +114,10 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
     if out is None:
         out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
     lib = _lib.load()
-    rc = lib.sgcn_tshift_fwd(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(scale),
-                             _ptr(shift), _ptr(stats), B, C, H, W, stride, _stream(inp))
+    nb = 4 * (inp.numel() + out.numel())
+    with _timed("tshift_fwd", 0, nb, inp):
+        rc = lib.sgcn_tshift_fwd(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(scale),
+                                 _ptr(shift), _ptr(stats), B, C, H, W, stride, _stream(inp))
     _lib.check(rc, "sgcn_tshift_fwd")
     return out
 
@@ -75,9 +137,11 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     gy = torch.empty((C,), device=dev, dtype=_F32)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
-    rc = lib.sgcn_tshift_bwd(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos), _ptr(scale),
-                             _ptr(shift), int(bool(relu_mask)), _ptr(gin), _ptr(gx), _ptr(gy),
-                             _ptr(ws), nbytes, B, C, H, W, stride, _stream(inp))
+    nb = 4 * (gout.numel() + 2 * inp.numel())
+    with _timed("tshift_bwd", 0, nb, inp):
+        rc = lib.sgcn_tshift_bwd(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos), _ptr(scale),
+                                 _ptr(shift), int(bool(relu_mask)), _ptr(gin), _ptr(gx),
+                                 _ptr(gy), _ptr(ws), nbytes, B, C, H, W, stride, _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd")
     return gin, gx, gy
 
@@ -106,10 +170,12 @@ def pw_fwd(w, w_mcontig, bias, x: PlaneView, out: PlaneView, M, K, T, V, mask=No
     _opt(bias, "bias"), _opt(mask, "mask")
     B = x.t.shape[0]
     lib = _lib.load()
-    rc = lib.sgcn_pw_fwd(_ptr(w), int(w_mcontig), _ptr(bias), _ptr(x.t), x.bstride, x.cstride,
-                         x.tstride, x.rsign, _ptr(mask), _ptr(out.t), out.bstride, out.cstride,
-                         out.tstride, out.rsign, int(relu), int(accumulate), B, M, K, T, V,
-                         _stream(x.t))
+    P = B * T * V
+    with _timed("pw_fwd", 2.0 * P * M * K, 4.0 * P * (M * (2 if accumulate else 1) + K), x.t):
+        rc = lib.sgcn_pw_fwd(_ptr(w), int(w_mcontig), _ptr(bias), _ptr(x.t), x.bstride,
+                             x.cstride, x.tstride, x.rsign, _ptr(mask), _ptr(out.t),
+                             out.bstride, out.cstride, out.tstride, out.rsign, int(relu),
+                             int(accumulate), B, M, K, T, V, _stream(x.t))
     _lib.check(rc, "sgcn_pw_fwd")
     return out.t
 
@@ -122,10 +188,13 @@ def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=Fals
     lib = _lib.load()
     nbytes = lib.sgcn_pw_dw_ws_bytes(B, M, Nc, T, V)
     ws = torch.empty((nbytes + 3) // 4, device=g.t.device, dtype=_F32)
-    rc = lib.sgcn_pw_dw(_ptr(g.t), g.bstride, g.cstride, g.tstride, g.rsign, _ptr(x.t),
-                        x.bstride, x.cstride, x.tstride, x.rsign, _ptr(mask), _ptr(dw),
-                        int(transpose), int(accumulate), _ptr(dbias), int(dbias_accumulate),
-                        _ptr(ws), nbytes, B, M, Nc, T, V, _stream(g.t))
+    P = B * T * V
+    with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t):
+        rc = lib.sgcn_pw_dw(_ptr(g.t), g.bstride, g.cstride, g.tstride, g.rsign, _ptr(x.t),
+                            x.bstride, x.cstride, x.tstride, x.rsign, _ptr(mask), _ptr(dw),
+                            int(transpose), int(accumulate), _ptr(dbias),
+                            int(dbias_accumulate), _ptr(ws), nbytes, B, M, Nc, T, V,
+                            _stream(g.t))
     _lib.check(rc, "sgcn_pw_dw")
     return dw
 

@@ -255,6 +255,22 @@ def gen_models(ref_sg, out):
         out[f"model_{name}_step_param_sum"] = np.array(
             [float(p.detach().double().sum()) for pn, p in m.named_parameters()
              if p.dtype.is_floating_point])
+        # the same forward/backward in float64 (conditioning reference: model-level fp32
+        # gradients through 10 BN units at bs=2 differ from it by up to ~3e-3 even on the
+        # reference's own fp32 path)
+        with _cpu_construction():
+            m64 = ref_sg.Model(num_class=num_class, num_point=V, num_person=M,
+                               graph="fixture_graph.Graph")
+        formula.fill_state(m64, seed=97 + sum(map(ord, name)))
+        m64 = m64.double().train()
+        logits64 = m64(x.double())
+        torch.nn.functional.cross_entropy(logits64, labels).backward()
+        out[f"model_{name}_logits_train64"] = _np(logits64)
+        p64 = dict(m64.named_parameters())
+        out[f"model_{name}_grad_norm64"] = np.array([float(p64[n].grad.norm()) for n in names])
+        for n in names:
+            if n.endswith(("xpos", "ypos")):
+                out[f"model_{name}_grad64.{n}"] = _np(p64[n].grad)
 
 
 def main():
