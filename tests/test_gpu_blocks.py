@@ -195,11 +195,9 @@ def test_model_matches_golden_fixture(golden, case):
     # Bar: the HIP path is as close to the float64 reference as the fp32 reference is
     # (median within 2x, worst parameter within 2x of the reference's worst).
     ref32, ref64 = fx[f"model_{name}_grad_norm"], fx[f"model_{name}_grad_norm64"]
-    zero = np.array([zero_by_construction(n.rsplit(".", 1)[0].rsplit(".", 1)[-1] + "."
-                                          + n.rsplit(".", 1)[-1]) or
-                     n.endswith(("Linear_bias", "down.0.bias", "residual.conv.bias"))
+    zero = np.array([n.endswith(("Linear_bias", "down.0.bias", "residual.conv.bias"))
                      for n in names])
-    nz = ~zero
+    nz = ~zero & (ref64 > 0)      # xpos gradients are exactly 0 (x-shift is frozen)
     err_ours = np.abs(gnorm - ref64)[nz] / ref64[nz]
     err_ref = np.abs(ref32 - ref64)[nz] / ref64[nz]
     assert np.median(err_ours) <= 2 * np.median(err_ref) + 1e-5, (np.median(err_ours),
