@@ -20,64 +20,68 @@ namespace {
 
 constexpr int kThreads = 256;
 
-struct Welford {
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  __device__ __forceinline__ void add(float x) {
-    n += 1.f;
-    const float d = x - mean;
-    mean += d / n;
-    m2 += d * (x - mean);
-  }
-};
+constexpr int kU = 4;  // elements in flight per thread per loop trip (all loads clamped)
 
 // ------------------------------------------------------------------------------------
-// forward statistics
+// forward statistics: shifted sums per plane (or per joint), no per-element division
 // ------------------------------------------------------------------------------------
 // part[plane] = {mean, M2} over the plane (per_joint = 0), or part[plane*V + v] over t.
+// Shifted data (x - x_first) keeps sum/sum-of-squares well conditioned; the merge over
+// the batch is done in double by bn_finalize_kernel.
 template <bool PER_JOINT>
 __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restrict__ x,
                                                             float2* __restrict__ part, int T,
                                                             int V) {
-  __shared__ float sn[kThreads], sm[kThreads], s2[kThreads];
+  __shared__ float s1[kThreads], s2[kThreads], red[2 * kThreads / 64];
   const int plane = blockIdx.x;
   const int P = T * V;
   const float* __restrict__ xp = x + (size_t)plane * P;
-  Welford w;
+  const int i = threadIdx.x;
   if (PER_JOINT) {
     const int G = kThreads / V;  // row groups
-    const int i = threadIdx.x;
+    float a = 0.f, q = 0.f;
+    const int v = i % V, r = i / V;
+    const float k0 = xp[v];      // shift: first row of this joint
     if (i < G * V) {
-      const int v = i % V, r = i / V;
-      for (int t = r; t < T; t += G) w.add(xp[t * V + v]);
+      for (int t0 = r; t0 < T; t0 += G * kU) {
+        float xv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) xv[u] = xp[min(t0 + u * G, T - 1) * V + v];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const float d = (t0 + u * G < T) ? xv[u] - k0 : 0.f;
+          a += d;
+          q += d * d;
+        }
+      }
     }
-    sn[i] = w.n; sm[i] = w.mean; s2[i] = w.m2;
+    s1[i] = a;
+    s2[i] = q;
     __syncthreads();
     if (i < V) {
-      Moments m{0.0, 0.0, 0.0};
-      for (int g = 0; g < G; ++g) {
-        const int j = g * V + i;
-        m = merge(m, {(double)sn[j], (double)sm[j], (double)s2[j]});
-      }
-      part[(size_t)plane * V + i] = make_float2((float)m.mean, (float)m.m2);
+      float ta = 0.f, tq = 0.f;
+      for (int g = 0; g < G; ++g) { ta += s1[g * V + i]; tq += s2[g * V + i]; }
+      const float n = (float)T;
+      part[(size_t)plane * V + i] = make_float2(xp[i] + ta / n, tq - ta * ta / n);
     }
   } else {
-    for (int o = threadIdx.x; o < P; o += kThreads) w.add(xp[o]);
-    sn[threadIdx.x] = w.n; sm[threadIdx.x] = w.mean; s2[threadIdx.x] = w.m2;
-    __syncthreads();
-    // tree merge in float pairs then double at the top 64
-    for (int s = kThreads / 2; s >= 64; s >>= 1) {
-      if (threadIdx.x < s) {
-        const int j = threadIdx.x + s;
-        const Moments m = merge({(double)sn[threadIdx.x], (double)sm[threadIdx.x], (double)s2[threadIdx.x]},
-                                {(double)sn[j], (double)sm[j], (double)s2[j]});
-        sn[threadIdx.x] = (float)m.n; sm[threadIdx.x] = (float)m.mean; s2[threadIdx.x] = (float)m.m2;
+    const float k0 = xp[0];
+    float a = 0.f, q = 0.f;
+    for (int base = 0; base < P; base += kThreads * kU) {
+      float xv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) xv[u] = xp[min(base + u * kThreads + i, P - 1)];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const float d = (base + u * kThreads + i < P) ? xv[u] - k0 : 0.f;
+        a += d;
+        q += d * d;
       }
-      __syncthreads();
     }
-    if (threadIdx.x == 0) {
-      Moments m{0.0, 0.0, 0.0};
-      for (int j = 0; j < 64; ++j) m = merge(m, {(double)sn[j], (double)sm[j], (double)s2[j]});
-      part[plane] = make_float2((float)m.mean, (float)m.m2);
+    block_sum2(a, q, red);
+    if (i == 0) {
+      const float n = (float)P;
+      part[plane] = make_float2(k0 + a / n, q - a * a / n);
     }
   }
 }
@@ -89,26 +93,51 @@ __device__ __forceinline__ int ref_feature(int f, int perm_V, int F) {
   return v * D + d;  // BatchNorm1d(V*C) feature index of (d, v)  (shift_gcn.py:135-137)
 }
 
-// part layout [B][C][J] (J = V if per-joint else 1); feature f = c*J + j; each partial
-// covers n_part elements.
-__global__ void bn_finalize_kernel(const float2* __restrict__ part, int B, int F, int n_part,
-                                   int perm_V, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float eps, float momentum,
-                                   float* __restrict__ running_mean,
-                                   float* __restrict__ running_var,
-                                   long long* __restrict__ num_batches,
-                                   float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                   float* __restrict__ scale_out, float* __restrict__ shift_out) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f == 0 && num_batches) *num_batches += 1;
-  if (f >= F) return;
-  Moments m{0.0, 0.0, 0.0};
-  for (int b = 0; b < B; ++b) {
-    const float2 p = part[(size_t)b * F + f];
-    m = merge(m, {(double)n_part, (double)p.x, (double)p.y});
+// Per-feature sums over the batch of float2 partials, parallel over b: block = 32
+// features x 8 batch slices; the 8 slice sums are added in fixed order (deterministic).
+// Returns the three double sums (x, y, x*x) in the q == 0 threads.
+constexpr int kFeat = 32, kSlices = 8;
+__device__ __forceinline__ bool feature_sums(const float2* __restrict__ part, int B, int F,
+                                             double& sx, double& sy, double& sxx, int& f) {
+  __shared__ double lx[kSlices][kFeat], ly[kSlices][kFeat], lxx[kSlices][kFeat];
+  const int fl = threadIdx.x % kFeat, q = threadIdx.x / kFeat;
+  f = blockIdx.x * kFeat + fl;
+  const int fc = min(f, F - 1);
+  double ax = 0.0, ay = 0.0, axx = 0.0;
+  for (int b = q; b < B; b += kSlices) {
+    const float2 p = part[(size_t)b * F + fc];
+    ax += p.x;
+    ay += p.y;
+    axx += (double)p.x * p.x;
   }
-  const double var = m.n > 0 ? m.m2 / m.n : 0.0;
-  const float mean = (float)m.mean;
+  lx[q][fl] = ax;
+  ly[q][fl] = ay;
+  lxx[q][fl] = axx;
+  __syncthreads();
+  if (q != 0 || f >= F) return false;
+  sx = sy = sxx = 0.0;
+  for (int k = 0; k < kSlices; ++k) { sx += lx[k][fl]; sy += ly[k][fl]; sxx += lxx[k][fl]; }
+  return true;
+}
+
+// part layout [B][F] of {mean, M2}, each over n_part elements. Equal counts, so
+// mean = avg(mean_b), M2 = sum M2_b + n_part * sum (mean_b - mean)^2 (double).
+__global__ __launch_bounds__(kFeat * kSlices) void bn_finalize_kernel(
+    const float2* __restrict__ part, int B, int F, int n_part, int perm_V,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
+    long long* __restrict__ num_batches, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale_out,
+    float* __restrict__ shift_out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += 1;
+  double smean, sm2, smean2;
+  int f;
+  if (!feature_sums(part, B, F, smean, sm2, smean2, f)) return;
+  const double nb = (double)B, np_ = (double)n_part, n = nb * np_;
+  const double mean_d = smean / nb;
+  const double m2 = sm2 + np_ * (smean2 - smean * smean / nb);
+  const double var = n > 0 ? fmax(m2, 0.0) / n : 0.0;
+  const float mean = (float)mean_d;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const int rf = ref_feature(f, perm_V, F);
   const float g = gamma ? gamma[rf] : 1.f;
@@ -119,7 +148,7 @@ __global__ void bn_finalize_kernel(const float2* __restrict__ part, int B, int F
   scale_out[f] = scale;
   shift_out[f] = bb - mean * scale;
   if (running_mean) {
-    const double unbiased = m.n > 1 ? m.m2 / (m.n - 1.0) : var;
+    const double unbiased = n > 1 ? fmax(m2, 0.0) / (n - 1.0) : var;
     running_mean[rf] = (1.f - momentum) * running_mean[rf] + momentum * mean;
     running_var[rf] = (1.f - momentum) * running_var[rf] + momentum * (float)unbiased;
   }
@@ -156,18 +185,29 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
   float sc = 0.f, sh = 0.f, rsc = 1.f, rsh = 0.f;
   if (!PER_JOINT) { sc = scale[c]; sh = shift[c]; }
   if (RES == 2) { rsc = rscale[c]; rsh = rshift[c]; }
-  int v = threadIdx.x % V;
   const int dv = kThreads % V;
-  for (int o = threadIdx.x; o < P; o += kThreads) {
-    float a = x[off + o];
-    if (PER_JOINT) a = a * scale[c * V + v] + shift[c * V + v];
-    else a = a * sc + sh;
-    if (RES == 1) a += r[off + o];
-    if (RES == 2) a += r[off + o] * rsc + rsh;
-    if (RELU) a = fmaxf(a, 0.f);
-    y[off + o] = a;
-    v += dv;
-    if (v >= V) v -= V;
+  int v = threadIdx.x % V;
+  for (int base = 0; base < P; base += kThreads * kU) {
+    float xv[kU], rv[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int oc = min(base + u * kThreads + (int)threadIdx.x, P - 1);
+      xv[u] = x[off + oc];
+      if (RES) rv[u] = r[off + oc];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int o = base + u * kThreads + threadIdx.x;
+      float a = xv[u];
+      if (PER_JOINT) a = a * scale[c * V + v] + shift[c * V + v];
+      else a = a * sc + sh;
+      if (RES == 1) a += rv[u];
+      if (RES == 2) a += rv[u] * rsc + rsh;
+      if (RELU) a = fmaxf(a, 0.f);
+      if (o < P) y[off + o] = a;
+      v += dv;
+      if (v >= V) v -= V;
+    }
   }
 }
 
@@ -185,26 +225,39 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
   const size_t off = (size_t)plane * P;
+  const int i = threadIdx.x;
   float rm = 0.f, ri = 0.f;
   if (RESBN) { rm = rmean[c]; ri = rinvstd[c]; }
   float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
   if (PER_JOINT) {
     const int G = kThreads / V;
-    const int i = threadIdx.x;
+    const int v = i % V, rr = i / V;
+    const int vc = min(v, V - 1);
+    const float mu = mean[c * V + vc], is = invstd[c * V + vc];
     if (i < G * V) {
-      const int v = i % V, rr = i / V;
-      const float mu = mean[c * V + v], is = invstd[c * V + v];
-      for (int t = rr; t < T; t += G) {
-        const int o = t * V + v;
-        float g = dy[off + o];
-        if (RELU) g = y[off + o] > 0.f ? g : 0.f;
-        a0 += g;
-        a1 += g * ((x[off + o] - mu) * is);
-        if (RESBN) { b0 += g; b1 += g * ((r[off + o] - rm) * ri); }
+      for (int t0 = rr; t0 < T; t0 += G * kU) {
+        float gv[kU], yv[kU], xv[kU], rv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int o = min(t0 + u * G, T - 1) * V + v;
+          gv[u] = dy[off + o];
+          if (RELU) yv[u] = y[off + o];
+          xv[u] = x[off + o];
+          if (RESBN) rv[u] = r[off + o];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          float g = (t0 + u * G < T) ? gv[u] : 0.f;
+          if (RELU) g = yv[u] > 0.f ? g : 0.f;
+          a0 += g;
+          a1 += g * ((xv[u] - mu) * is);
+          if (RESBN) { b0 += g; b1 += g * ((rv[u] - rm) * ri); }
+        }
       }
     }
     if (RESBN) block_sum2(b0, b1, red);
-    s0[i] = a0; s1[i] = a1;
+    s0[i] = a0;
+    s1[i] = a1;
     __syncthreads();
     if (i < V) {
       float t0 = 0.f, t1 = 0.f;
@@ -214,16 +267,28 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     if (RESBN && i == 0) rpart[plane] = make_float2(b0, b1);
   } else {
     const float mu = mean[c], is = invstd[c];
-    for (int o = threadIdx.x; o < P; o += kThreads) {
-      float g = dy[off + o];
-      if (RELU) g = y[off + o] > 0.f ? g : 0.f;
-      a0 += g;
-      a1 += g * ((x[off + o] - mu) * is);
-      if (RESBN) { b0 += g; b1 += g * ((r[off + o] - rm) * ri); }
+    for (int base = 0; base < P; base += kThreads * kU) {
+      float gv[kU], yv[kU], xv[kU], rv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int o = min(base + u * kThreads + i, P - 1);
+        gv[u] = dy[off + o];
+        if (RELU) yv[u] = y[off + o];
+        xv[u] = x[off + o];
+        if (RESBN) rv[u] = r[off + o];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        float g = (base + u * kThreads + i < P) ? gv[u] : 0.f;
+        if (RELU) g = yv[u] > 0.f ? g : 0.f;
+        a0 += g;
+        a1 += g * ((xv[u] - mu) * is);
+        if (RESBN) { b0 += g; b1 += g * ((rv[u] - rm) * ri); }
+      }
     }
     block_sum2(a0, a1, red);
     if (RESBN) block_sum2(b0, b1, red);
-    if (threadIdx.x == 0) {
+    if (i == 0) {
       part[plane] = make_float2(a0, a1);
       if (RESBN) rpart[plane] = make_float2(b0, b1);
     }
@@ -232,29 +297,22 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
 
 // dgamma = sum g*xhat, dbeta = sum g; dx = k1*g + k2*x + k3 with
 // k1 = gamma*invstd, k2 = -k1*invstd*mean(g*xhat), k3 = -k1*mean(g) - k2*mean_x
-__global__ void bn_bwd_finalize_kernel(const float2* __restrict__ part, int B, int F,
-                                       float n_total, int perm_V,
-                                       const float* __restrict__ mean,
-                                       const float* __restrict__ invstd,
-                                       const float* __restrict__ gamma,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       int accumulate, float* __restrict__ coef) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= F) return;
-  double sg = 0.0, sgx = 0.0;
-  for (int b = 0; b < B; ++b) {
-    const float2 p = part[(size_t)b * F + f];
-    sg += p.x;
-    sgx += p.y;
-  }
+__global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
+    const float2* __restrict__ part, int B, int F, double n_total, int perm_V,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    int accumulate, float* __restrict__ coef) {
+  double sg, sgx, unused;
+  int f;
+  if (!feature_sums(part, B, F, sg, sgx, unused, f)) return;
   const int rf = ref_feature(f, perm_V, F);
   if (dgamma) dgamma[rf] = accumulate ? dgamma[rf] + (float)sgx : (float)sgx;
   if (dbeta) dbeta[rf] = accumulate ? dbeta[rf] + (float)sg : (float)sg;
   const float g = gamma ? gamma[rf] : 1.f;
   const float is = invstd[f];
   const float k1 = g * is;
-  const float k2 = (float)(-(double)k1 * (double)is * (sgx / (double)n_total));
-  const float k3 = (float)(-(double)k1 * (sg / (double)n_total) - (double)k2 * (double)mean[f]);
+  const float k2 = (float)(-(double)k1 * (double)is * (sgx / n_total));
+  const float k3 = (float)(-(double)k1 * (sg / n_total) - (double)k2 * (double)mean[f]);
   coef[f] = k1;
   coef[F + f] = k2;
   coef[2 * F + f] = k3;
@@ -273,20 +331,35 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   float k1 = 0.f, k2 = 0.f, k3 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
   if (!PER_JOINT) { k1 = coef[c]; k2 = coef[F + c]; k3 = coef[2 * F + c]; }
   if (RES == 2) { q1 = rcoef[c]; q2 = rcoef[RF + c]; q3 = rcoef[2 * RF + c]; }
-  int v = threadIdx.x % V;
   const int dv = kThreads % V;
-  for (int o = threadIdx.x; o < P; o += kThreads) {
-    float g = dy[off + o];
-    if (RELU) g = y[off + o] > 0.f ? g : 0.f;
-    if (PER_JOINT) {
-      const int f = c * V + v;
-      k1 = coef[f]; k2 = coef[F + f]; k3 = coef[2 * F + f];
+  int v = threadIdx.x % V;
+  for (int base = 0; base < P; base += kThreads * kU) {
+    float gv[kU], yv[kU], xv[kU], rv[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int o = min(base + u * kThreads + (int)threadIdx.x, P - 1);
+      gv[u] = dy[off + o];
+      if (RELU) yv[u] = y[off + o];
+      xv[u] = x[off + o];
+      if (RES == 2) rv[u] = r[off + o];
     }
-    dx[off + o] = k1 * g + k2 * x[off + o] + k3;
-    if (RES == 1) dr[off + o] = g;
-    if (RES == 2) dr[off + o] = q1 * g + q2 * r[off + o] + q3;
-    v += dv;
-    if (v >= V) v -= V;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int o = base + u * kThreads + threadIdx.x;
+      float g = gv[u];
+      if (RELU) g = yv[u] > 0.f ? g : 0.f;
+      if (PER_JOINT) {
+        const int f = c * V + v;
+        k1 = coef[f]; k2 = coef[F + f]; k3 = coef[2 * F + f];
+      }
+      if (o < P) {
+        dx[off + o] = k1 * g + k2 * xv[u] + k3;
+        if (RES == 1) dr[off + o] = g;
+        if (RES == 2) dr[off + o] = q1 * g + q2 * rv[u] + q3;
+      }
+      v += dv;
+      if (v >= V) v -= V;
+    }
   }
 }
 
@@ -295,6 +368,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
 // ------------------------------------------------------------------------------------
 // dx[b,c,t,v'] = dxt[b,c,t,u]*m[u][c] (+ add1 + add2), u = (v' - c) mod V  (index_select^T)
 // dmask_part[b][c][u] = sum_t dxt[b,c,t,u] * x0[b,c,t,(u+c) mod V]
+template <bool ADD1, bool ADD2>
 __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
     const float* __restrict__ dxt, const float* __restrict__ x0, const float* __restrict__ m,
     const float* __restrict__ add1, const float* __restrict__ add2, float* __restrict__ dx,
@@ -304,38 +378,64 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
   const int P = T * V;
   const size_t off = (size_t)plane * P;
   const int rc = c % V;
-  // scatter pass over destination positions v'
+  const int i = threadIdx.x;
+  // scatter pass over destination positions v' (each thread keeps v' = o mod V)
   {
-    int v = threadIdx.x % V;
     const int dv = kThreads % V;
-    for (int o = threadIdx.x; o < P; o += kThreads) {
-      int u = v - rc;
-      u = u < 0 ? u + V : u;
-      const int src = o - v + u;
-      float val = dxt[off + src] * m[u * C + c];
-      if (add1) val += add1[off + o];
-      if (add2) val += add2[off + o];
-      dx[off + o] = val;
-      v += dv;
-      if (v >= V) v -= V;
+    int v = i % V;
+    for (int base = 0; base < P; base += kThreads * kU) {
+      float gv[kU], a1[kU], a2[kU];
+      int uu[kU];
+      int vv = v;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int oraw = base + u * kThreads + i;
+        const int o = min(oraw, P - 1);
+        int uq = vv - rc;
+        uq = uq < 0 ? uq + V : uq;
+        uu[u] = uq;
+        gv[u] = dxt[off + min(oraw - vv + uq, P - 1)];
+        if (ADD1) a1[u] = add1[off + o];
+        if (ADD2) a2[u] = add2[off + o];
+        vv += dv;
+        if (vv >= V) vv -= V;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int o = base + u * kThreads + i;
+        float val = gv[u] * m[uu[u] * C + c];
+        if (ADD1) val += a1[u];
+        if (ADD2) val += a2[u];
+        if (o < P) dx[off + o] = val;
+      }
+      v = vv;
     }
   }
   // mask-gradient partials per u over t
   const int G = kThreads / V;
-  const int i = threadIdx.x;
   float acc = 0.f;
   if (i < G * V) {
     const int u = i % V, rr = i / V;
     int xv = u + rc;
     xv = xv >= V ? xv - V : xv;
-    for (int t = rr; t < T; t += G) acc += dxt[off + t * V + u] * x0[off + t * V + xv];
+    for (int t0 = rr; t0 < T; t0 += G * kU) {
+      float gv[kU], xq[kU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const int t = min(t0 + k * G, T - 1);
+        gv[k] = dxt[off + t * V + u];
+        xq[k] = x0[off + t * V + xv];
+      }
+#pragma unroll
+      for (int k = 0; k < kU; ++k) acc += (t0 + k * G < T) ? gv[k] * xq[k] : 0.f;
+    }
   }
   s0[i] = acc;
   __syncthreads();
   if (i < V) {
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += s0[g * V + i];
-    dmask_part[(size_t)plane * V + i] = s;
+    float sum = 0.f;
+    for (int g = 0; g < G; ++g) sum += s0[g * V + i];
+    dmask_part[(size_t)plane * V + i] = sum;
   }
 }
 
@@ -345,15 +445,24 @@ __global__ void mask_prep_kernel(const float* __restrict__ mask, float* __restri
   if (i < n) m[i] = tanhf(mask[i]) + 1.f;
 }
 
-// dmask[u][c] (+)= (sum_b part[b][c][u]) * (1 - tanh(mask)^2)
-__global__ void mask_grad_finalize_kernel(const float* __restrict__ part,
-                                          const float* __restrict__ mask, int B, int C, int V,
-                                          float* __restrict__ dmask, int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // i = u*C + c
-  if (i >= C * V) return;
-  const int u = i / C, c = i - u * C;
+// dmask[u][c] (+)= (sum_b part[b][c][u]) * (1 - tanh(mask)^2); parallel over b
+__global__ __launch_bounds__(kFeat * kSlices) void mask_grad_finalize_kernel(
+    const float* __restrict__ part, const float* __restrict__ mask, int B, int C, int V,
+    float* __restrict__ dmask, int accumulate) {
+  __shared__ double ls[kSlices][kFeat];
+  const int F = C * V;  // part feature f = c*V + u
+  const int fl = threadIdx.x % kFeat, q = threadIdx.x / kFeat;
+  const int f = blockIdx.x * kFeat + fl;
+  const int fc = min(f, F - 1);
+  double a = 0.0;
+  for (int b = q; b < B; b += kSlices) a += part[(size_t)b * F + fc];
+  ls[q][fl] = a;
+  __syncthreads();
+  if (q != 0 || f >= F) return;
   double s = 0.0;
-  for (int b = 0; b < B; ++b) s += part[((size_t)b * C + c) * V + u];
+  for (int k = 0; k < kSlices; ++k) s += ls[k][fl];
+  const int c = f / V, u = f - c * V;
+  const int i = u * C + c;
   const float t = tanhf(mask[i]);
   const float g = (float)s * (1.f - t * t);
   dmask[i] = accumulate ? dmask[i] + g : g;
@@ -393,7 +502,7 @@ int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
   SGCN_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
   hipStream_t st = (hipStream_t)stream;
-  bn_finalize_kernel<<<(F + 255) / 256, 256, 0, st>>>(
+  bn_finalize_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSlices, 0, st>>>(
       (const float2*)part, B, F, n_part, perm_V, gamma, beta, eps, momentum, running_mean,
       running_var, num_batches, mean, invstd, scale, shift);
   SGCN_LAUNCH_CHECK();
@@ -465,8 +574,8 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
                          void* stream) {
   SGCN_REQUIRE(part && B > 0 && F > 0 && n_total > 0 && mean && invstd && coef);
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
-  bn_bwd_finalize_kernel<<<(F + 255) / 256, 256, 0, (hipStream_t)stream>>>(
-      (const float2*)part, B, F, (float)n_total, perm_V, mean, invstd, gamma, dgamma, dbeta,
+  bn_bwd_finalize_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSlices, 0, (hipStream_t)stream>>>(
+      (const float2*)part, B, F, (double)n_total, perm_V, mean, invstd, gamma, dgamma, dbeta,
       accumulate, coef);
   SGCN_LAUNCH_CHECK();
   return 0;
@@ -508,8 +617,12 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(dxt && x0 && m && dx && dmask_part);
-  gcn_dx_finish_kernel<<<B * C, kThreads, 0, (hipStream_t)stream>>>(dxt, x0, m, add1, add2, dx,
-                                                                    dmask_part, C, T, V);
+  hipStream_t st = (hipStream_t)stream;
+#define SGCN_FIN(A1, A2) \
+  gcn_dx_finish_kernel<A1, A2><<<B * C, kThreads, 0, st>>>(dxt, x0, m, add1, add2, dx, dmask_part, C, T, V)
+  if (add1) { if (add2) SGCN_FIN(true, true); else SGCN_FIN(true, false); }
+  else { if (add2) SGCN_FIN(false, true); else SGCN_FIN(false, false); }
+#undef SGCN_FIN
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -517,8 +630,8 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
 int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,
                             float* dmask, int accumulate, void* stream) {
   SGCN_REQUIRE(part && mask && dmask && B > 0 && C > 0 && V > 0);
-  mask_grad_finalize_kernel<<<(C * V + 255) / 256, 256, 0, (hipStream_t)stream>>>(
-      part, mask, B, C, V, dmask, accumulate);
+  mask_grad_finalize_kernel<<<(C * V + kFeat - 1) / kFeat, kFeat * kSlices, 0,
+                              (hipStream_t)stream>>>(part, mask, B, C, V, dmask, accumulate);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

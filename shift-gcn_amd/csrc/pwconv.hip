@@ -21,7 +21,7 @@
 //      X tile run back to back (Infinity-Cache hits for the second M-tile).
 //  * pw_dw_kernel  : split-K dW[m][n] = sum_{b,p} G(b,m,p) * X(b,n,p) over all positions,
 //      deterministic fp32 partial slabs [split][M][N] + row sums (bias grad), reduced in
-//      fixed order by pw_dw_reduce_kernel (optionally transposed, for Linear_weight's
+//      fixed order by slab_reduce_kernel (optionally transposed, for Linear_weight's
 //      (C_in, C_out) layout).
 #include "common.hpp"
 
@@ -97,8 +97,9 @@ __global__ __launch_bounds__(kThreads) void pw_fwd_kernel(FwdArgs p) {
   const int nb = tid % BN, kb0 = tid / BN;
   const int n = n0 + nb;
   const bool nvalid = n < N;
-  const int tt = nvalid ? n / V : 0;
-  const int vv = nvalid ? n - tt * V : 0;
+  const int ncl = min(n, N - 1);           // clamped: loads stay in bounds, value masked
+  const int tt = ncl / V;
+  const int vv = ncl - tt * V;
   const float* xb = p.x.ptr + (long long)b * p.x.bstride + (long long)tt * p.x.tstride * V;
   // A staging
   const int am = p.a_mcontig ? tid % BM : tid / BK;
@@ -111,14 +112,12 @@ __global__ __launch_bounds__(kThreads) void pw_fwd_kernel(FwdArgs p) {
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int k = k0 + kb0 + i * (kThreads / BN);
-      float v = 0.f;
-      if (nvalid && k < K) {
-        int c = vv + rot_in[k];
-        c = c >= V ? c - V : c;
-        v = xb[(long long)k * p.x.cstride + c];
-        if (MASK) v *= p.mask[vv * K + k];
-      }
-      rb[i] = v;
+      const int kc = min(k, K - 1);
+      int c = vv + rot_in[kc];
+      c = c >= V ? c - V : c;
+      float v = xb[(long long)kc * p.x.cstride + c];
+      if (MASK) v *= p.mask[vv * K + kc];
+      rb[i] = (nvalid && k < K) ? v : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -126,10 +125,10 @@ __global__ __launch_bounds__(kThreads) void pw_fwd_kernel(FwdArgs p) {
       if (p.a_mcontig) { m = am; k = ak + i * A_KSTEP; }
       else { m = am + i * A_MSTEP; k = ak; }
       const int gm = m0 + m, gk = k0 + k;
-      float v = 0.f;
-      if (gm < M && gk < K)
-        v = p.a_mcontig ? p.A[(long long)gk * p.lda + gm] : p.A[(long long)gm * p.lda + gk];
-      ra[i] = v;
+      const int gmc = min(gm, M - 1), gkc = min(gk, K - 1);
+      const float v = p.a_mcontig ? p.A[(long long)gkc * p.lda + gmc]
+                                  : p.A[(long long)gmc * p.lda + gkc];
+      ra[i] = (gm < M && gk < K) ? v : 0.f;
     }
   };
   auto store_stage = [&]() {
@@ -212,7 +211,7 @@ struct DwArgs {
   int chunks_per_split;
 };
 
-template <int BM, int BN>
+template <int BM, int BN, bool MASK>
 __global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
   constexpr int BK = 32;
   constexpr int MI = BM / 64, NJ = BN / 64;
@@ -248,32 +247,29 @@ __global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
     const int b = q / nchunk;
     const int n = (q - b * nchunk) * BK + kq;
     const bool nvalid = n < N;
-    const int t = nvalid ? n / V : 0;
-    const int v = nvalid ? n - t * V : 0;
+    const int ncl = min(n, N - 1);
+    const int t = ncl / V;
+    const int v = ncl - t * V;
     const float* gb = p.g.ptr + (long long)b * p.g.bstride + (long long)t * p.g.tstride * V;
     const float* xb = p.x.ptr + (long long)b * p.x.bstride + (long long)t * p.x.tstride * V;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int row = r0 + i * RSTEP, m = m0 + row;
-      float val = 0.f;
-      if (nvalid && m < p.M) {
-        int c = v + rot_g[row];
-        c = c >= V ? c - V : c;
-        val = gb[(long long)m * p.g.cstride + c];
-      }
-      ra[i] = val;
+      const int mc = min(m, p.M - 1);
+      int c = v + rot_g[row];
+      c = c >= V ? c - V : c;
+      const float val = gb[(long long)mc * p.g.cstride + c];
+      ra[i] = (nvalid && m < p.M) ? val : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int row = r0 + i * RSTEP, c = c0 + row;
-      float val = 0.f;
-      if (nvalid && c < p.Nc) {
-        int cc = v + rot_x[row];
-        cc = cc >= V ? cc - V : cc;
-        val = xb[(long long)c * p.x.cstride + cc];
-        if (p.mask) val *= p.mask[v * p.Nc + c];
-      }
-      rb[i] = val;
+      const int ccl = min(c, p.Nc - 1);
+      int cc = v + rot_x[row];
+      cc = cc >= V ? cc - V : cc;
+      float val = xb[(long long)ccl * p.x.cstride + cc];
+      if (MASK) val *= p.mask[v * p.Nc + ccl];
+      rb[i] = (nvalid && c < p.Nc) ? val : 0.f;
     }
   };
 
@@ -337,24 +333,34 @@ __global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
   }
 }
 
-// out[m][n] (or out[n][m] if transpose) (+)= sum_s slab[s][m][n]; bias[m] (+)= sum_s bslab
-__global__ void pw_dw_reduce_kernel(const float* __restrict__ slab,
-                                    const float* __restrict__ bslab, int S, int M, int Nc,
-                                    float* __restrict__ out, int transpose, int accum,
-                                    float* __restrict__ bias_out, int bias_accum) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  const int MN = M * Nc;
-  if (idx < MN) {
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += slab[(size_t)k * MN + idx];
-    const int m = idx / Nc, n = idx - m * Nc;
-    float* d = transpose ? out + (size_t)n * M + m : out + idx;
-    *d = accum ? *d + s : s;
+// out[i] (+)= sum_s slab[s*n + i], i < n, in a FIXED order (deterministic): 64 outputs
+// per block, 4 split-groups of 64 threads each summing every 4th split with 8 loads in
+// flight, then the 4 group sums added in order. transpose: i = m*Nc + c -> out[c*M + m].
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab,
+                                                          int S, int n, int M, int Nc,
+                                                          float* __restrict__ out,
+                                                          int transpose, int accum) {
+  __shared__ float red[4][64];
+  const int il = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + il;
+  const int ic = min(i, n - 1);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = q;
+  for (; s + 28 < S; s += 32) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += slab[(size_t)(s + 4 * k) * n + ic];
   }
-  if (bias_out && idx < M) {
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += bslab[(size_t)k * M + idx];
-    bias_out[idx] = bias_accum ? bias_out[idx] + s : s;
+  for (; s < S; s += 4) acc[0] += slab[(size_t)s * n + ic];
+  red[q][il] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (q == 0 && i < n) {
+    const float tot = (red[0][il] + red[1][il]) + (red[2][il] + red[3][il]);
+    int dst = i;
+    if (transpose) {
+      const int m = i / Nc, c = i - m * Nc;
+      dst = c * M + m;
+    }
+    out[dst] = accum ? out[dst] + tot : tot;
   }
 }
 
@@ -376,9 +382,10 @@ void launch_fwd_bm(const FwdArgs& a, int B, bool mask, bool relu, bool accum, hi
 }
 
 int dw_splits(int M, int Nc, int B, int N, int tiles) {
+  // ~512 workgroups (2 per CU at this kernel's register budget); slab <= 16 MiB
   const int total = B * ((N + 31) / 32);
-  int S = (1024 + tiles - 1) / tiles;
-  const long long cap = (32LL << 20) / (4LL * M * Nc);  // slab <= 32 MiB
+  int S = (512 + tiles - 1) / tiles;
+  const long long cap = (16LL << 20) / (4LL * M * Nc);
   if (S > cap) S = (int)cap;
   if (S > total) S = total;
   return S < 1 ? 1 : S;
@@ -461,15 +468,24 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
   a.chunks_per_split = (total + S - 1) / S;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(tiles, S);
-  if (bm == 128 && bn == 128) pw_dw_kernel<128, 128><<<grid, kThreads, 0, st>>>(a);
-  else if (bm == 128) pw_dw_kernel<128, 64><<<grid, kThreads, 0, st>>>(a);
-  else if (bn == 128) pw_dw_kernel<64, 128><<<grid, kThreads, 0, st>>>(a);
-  else pw_dw_kernel<64, 64><<<grid, kThreads, 0, st>>>(a);
+#define SGCN_DW(BM_, BN_)                                                       \
+  (mask ? pw_dw_kernel<BM_, BN_, true><<<grid, kThreads, 0, st>>>(a)           \
+        : pw_dw_kernel<BM_, BN_, false><<<grid, kThreads, 0, st>>>(a))
+  if (bm == 128 && bn == 128) SGCN_DW(128, 128);
+  else if (bm == 128) SGCN_DW(128, 64);
+  else if (bn == 128) SGCN_DW(64, 128);
+  else SGCN_DW(64, 64);
+#undef SGCN_DW
   SGCN_LAUNCH_CHECK();
   const int MN = M * Nc;
-  pw_dw_reduce_kernel<<<(max(MN, M) + 255) / 256, 256, 0, st>>>(
-      a.slab, a.bslab, S, M, Nc, dw, dw_transpose, dw_accumulate, dbias, dbias_accumulate);
+  slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(a.slab, S, MN, M, Nc, dw, dw_transpose,
+                                                    dw_accumulate);
   SGCN_LAUNCH_CHECK();
+  if (dbias) {
+    slab_reduce_kernel<<<(M + 63) / 64, 256, 0, st>>>(a.bslab, S, M, M, 1, dbias, 0,
+                                                     dbias_accumulate);
+    SGCN_LAUNCH_CHECK();
+  }
   return 0;
 }
 

@@ -72,11 +72,17 @@ struct Walker {
   }
 };
 
+// Branch-free tap: the load always reads an in-bounds (clamped) address and the value
+// is selected to 0 afterwards, so hipcc never branches around a load (a branch per tap
+// makes it wait vmcnt(0) per element: latency-bound, measured ~1.5 TB/s).
 template <bool AFFINE>
-__device__ __forceinline__ float tap(const float* __restrict__ p, bool ok, float a, float b) {
-  if (!ok) return 0.f;
-  const float v = *p;
-  return AFFINE ? v * a + b : v;
+__device__ __forceinline__ float tap(const float* __restrict__ plane, int r, int c, int H,
+                                     int W, float a, float b) {
+  const bool ok = (unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W;
+  const int rr = min(max(r, 0), H - 1), cc = min(max(c, 0), W - 1);
+  float v = plane[rr * W + cc];
+  if (AFFINE) v = v * a + b;
+  return ok ? v : 0.f;
 }
 
 // ------------------------------------------------------------------------------------
@@ -106,20 +112,15 @@ __global__ __launch_bounds__(kThreads) void tshift_fwd_kernel(
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const int o = base + e * kThreads + threadIdx.x;
-      v[e] = 0.f;
-      if (o < n) {
-        const int r1 = pos.h * stride + g.y1;
-        const int c1 = pos.w + g.x1;
-        const bool rv1 = (unsigned)r1 < (unsigned)Hb, rv2 = (unsigned)(r1 + 1) < (unsigned)Hb;
-        const bool cv1 = (unsigned)c1 < (unsigned)W, cv2 = (unsigned)(c1 + 1) < (unsigned)W;
-        const float* p = src + (ptrdiff_t)r1 * W + c1;
-        const float q11 = tap<AFFINE>(p, rv1 && cv1, a, b);
-        const float q21 = tap<AFFINE>(p + 1, rv1 && cv2, a, b);
-        const float q12 = tap<AFFINE>(p + W, rv2 && cv1, a, b);
-        const float q22 = tap<AFFINE>(p + W + 1, rv2 && cv2, a, b);
-        v[e] = blend(q11, q21, q12, q22, g.dx, g.dy);
-        dst[o] = v[e];
-      }
+      const int r1 = pos.h * stride + g.y1;
+      const int c1 = pos.w + g.x1;
+      const float q11 = tap<AFFINE>(src, r1, c1, Hb, W, a, b);
+      const float q21 = tap<AFFINE>(src, r1, c1 + 1, Hb, W, a, b);
+      const float q12 = tap<AFFINE>(src, r1 + 1, c1, Hb, W, a, b);
+      const float q22 = tap<AFFINE>(src, r1 + 1, c1 + 1, Hb, W, a, b);
+      const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
+      v[e] = o < n ? val : 0.f;
+      if (o < n) dst[o] = val;
       pos.next();
     }
     if (STATS) {
@@ -168,7 +169,9 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
 
   // (1) grad_input over the bottom grid: bilinear sample of grad_output at (-x, -y)
   //     (.cu:108-150 stride 1; .cu:191-254 stride 2 with the even-row rule)
-  {
+  if (Ho == 0) {  // empty top grid: every tap is out of range (and must not be read)
+    for (int o = threadIdx.x; o < Hb * W; o += kThreads) gi[o] = 0.f;
+  } else {
     const Geom r = make_geom(-x, -y);
     const int nb = Hb * W;
     for (int base = 0; base < nb; base += EPT * kThreads) {
@@ -176,37 +179,28 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < EPT; ++e) {
         const int o = base + e * kThreads + threadIdx.x;
-        if (o < nb) {
-          const int h1 = pos.h + r.y1, h2 = h1 + 1;
-          const int w1 = pos.w + r.x1, w2 = w1 + 1;
-          const bool cv1 = (unsigned)w1 < (unsigned)W, cv2 = (unsigned)w2 < (unsigned)W;
-          float q11 = 0.f, q21 = 0.f, q12 = 0.f, q22 = 0.f;
-          if (STRIDE == 1) {
-            const bool rv1 = (unsigned)h1 < (unsigned)Ho, rv2 = (unsigned)h2 < (unsigned)Ho;
-            const float* p = go + (ptrdiff_t)h1 * W + w1;
-            if (rv1 && cv1) q11 = p[0];
-            if (rv1 && cv2) q21 = p[1];
-            if (rv2 && cv1) q12 = p[W];
-            if (rv2 && cv2) q22 = p[W + 1];
-          } else {
-            // h_im % 2 == 0 (C++ remainder), then h_im / 2 (truncation), bounds on top grid
-            if (h1 % 2 == 0) {
-              const int hq = h1 / 2;
-              const bool rv = hq >= 0 && hq < Ho;
-              if (rv && cv1) q11 = go[hq * W + w1];
-              if (rv && cv2) q21 = go[hq * W + w2];
-            }
-            if (h2 % 2 == 0) {
-              const int hq = h2 / 2;
-              const bool rv = hq >= 0 && hq < Ho;
-              if (rv && cv1) q12 = go[hq * W + w1];
-              if (rv && cv2) q22 = go[hq * W + w2];
-            }
-          }
-          float val = blend(q11, q21, q12, q22, r.dx, r.dy);
-          if (RELU_MASK) val = src[o] > 0.f ? val : 0.f;
-          gi[o] = val;
+        const int h1 = pos.h + r.y1, h2 = h1 + 1;
+        const int w1 = pos.w + r.x1, w2 = w1 + 1;
+        float q11, q21, q12, q22;
+        if (STRIDE == 1) {
+          q11 = tap<false>(go, h1, w1, Ho, W, 1.f, 0.f);
+          q21 = tap<false>(go, h1, w2, Ho, W, 1.f, 0.f);
+          q12 = tap<false>(go, h2, w1, Ho, W, 1.f, 0.f);
+          q22 = tap<false>(go, h2, w2, Ho, W, 1.f, 0.f);
+        } else {
+          // h_im % 2 == 0 (C++ remainder), then h_im / 2 (truncation), bounds on top grid;
+          // odd h_im -> row index -1 (rejected by the bounds test)
+          const int hq1 = (h1 % 2 == 0) ? h1 / 2 : -1;
+          const int hq2 = (h2 % 2 == 0) ? h2 / 2 : -1;
+          q11 = tap<false>(go, hq1, w1, Ho, W, 1.f, 0.f);
+          q21 = tap<false>(go, hq1, w2, Ho, W, 1.f, 0.f);
+          q12 = tap<false>(go, hq2, w1, Ho, W, 1.f, 0.f);
+          q22 = tap<false>(go, hq2, w2, Ho, W, 1.f, 0.f);
         }
+        float val = blend(q11, q21, q12, q22, r.dx, r.dy);
+        const int oc = min(o, nb - 1);
+        if (RELU_MASK) val = src[oc] > 0.f ? val : 0.f;
+        if (o < nb) gi[o] = val;
         pos.next();
       }
     }
@@ -222,22 +216,17 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < EPT; ++e) {
         const int o = base + e * kThreads + threadIdx.x;
-        if (o < nt) {
-          const int r1 = pos.h * STRIDE + g.y1;
-          const int c1 = pos.w + g.x1;
-          const bool rv1 = (unsigned)r1 < (unsigned)Hb, rv2 = (unsigned)(r1 + 1) < (unsigned)Hb;
-          const bool cv1 = (unsigned)c1 < (unsigned)W, cv2 = (unsigned)(c1 + 1) < (unsigned)W;
-          const float* p = src + (ptrdiff_t)r1 * W + c1;
-          const float q11 = tap<AFFINE>(p, rv1 && cv1, a, b);
-          const float q21 = tap<AFFINE>(p + 1, rv1 && cv2, a, b);
-          const float q12 = tap<AFFINE>(p + W, rv2 && cv1, a, b);
-          const float q22 = tap<AFFINE>(p + W + 1, rv2 && cv2, a, b);
-          const float vx = (1.f - g.dy) * (q21 - q11) + g.dy * (q22 - q12);
-          const float vy = (1.f - g.dx) * (q12 - q11) + g.dx * (q22 - q21);
-          const float gv = go[o];
-          ax += vx * gv;
-          ay += vy * gv;
-        }
+        const int r1 = pos.h * STRIDE + g.y1;
+        const int c1 = pos.w + g.x1;
+        const float q11 = tap<AFFINE>(src, r1, c1, Hb, W, a, b);
+        const float q21 = tap<AFFINE>(src, r1, c1 + 1, Hb, W, a, b);
+        const float q12 = tap<AFFINE>(src, r1 + 1, c1, Hb, W, a, b);
+        const float q22 = tap<AFFINE>(src, r1 + 1, c1 + 1, Hb, W, a, b);
+        const float vx = (1.f - g.dy) * (q21 - q11) + g.dy * (q22 - q12);
+        const float vy = (1.f - g.dx) * (q12 - q11) + g.dx * (q22 - q21);
+        const float gv = o < nt ? go[min(o, nt - 1)] : 0.f;
+        ax += vx * gv;
+        ay += vy * gv;
         pos.next();
       }
     }
@@ -250,16 +239,26 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
 // up to rounding), then applyShiftConstraint (.cu:370-395) with its float/double
 // promotions: sqrt(dy*dy) in float (correctly rounded), quotients in float, times the
 // double literals 0.0 / 0.01, stored as float; the dr == 0 branch stores 0.0 / 0.0001.
-__global__ void tshift_pos_finalize_kernel(const float2* __restrict__ pgrad, int B, int C,
-                                           float* __restrict__ gx, float* __restrict__ gy) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sx = 0.0, sy = 0.0;
-  for (int b = 0; b < B; ++b) {
-    const float2 p = pgrad[(size_t)b * C + c];
-    sx += (double)p.x;
-    sy += (double)p.y;
+__global__ __launch_bounds__(256) void tshift_pos_finalize_kernel(
+    const float2* __restrict__ pgrad, int B, int C, float* __restrict__ gx,
+    float* __restrict__ gy) {
+  // 32 channels x 8 batch slices per block; slices added in fixed order
+  __shared__ double lx[8][32], ly[8][32];
+  const int cl = threadIdx.x % 32, q = threadIdx.x / 32;
+  const int c = blockIdx.x * 32 + cl;
+  const int cc = min(c, C - 1);
+  double ax = 0.0, ay = 0.0;
+  for (int b = q; b < B; b += 8) {
+    const float2 p = pgrad[(size_t)b * C + cc];
+    ax += (double)p.x;
+    ay += (double)p.y;
   }
+  lx[q][cl] = ax;
+  ly[q][cl] = ay;
+  __syncthreads();
+  if (q != 0 || c >= C) return;
+  double sx = 0.0, sy = 0.0;
+  for (int k = 0; k < 8; ++k) { sx += lx[k][cl]; sy += ly[k][cl]; }
   const float Gx = (float)(sx / (double)B);
   const float Gy = (float)(sy / (double)B);
   const float gy2 = Gy * Gy;
@@ -365,7 +364,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   if (ept == 8) SGCN_BWD_EPT(8); else if (ept == 16) SGCN_BWD_EPT(16); else SGCN_BWD_EPT(32);
 #undef SGCN_BWD_EPT
   SGCN_LAUNCH_CHECK();
-  tshift_pos_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(pg, B, C, gx, gy);
+  tshift_pos_finalize_kernel<<<(C + 31) / 32, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

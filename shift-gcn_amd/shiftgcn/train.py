@@ -27,9 +27,21 @@ def sgd_param_groups(model: torch.nn.Module, base_lr: float):
     return groups
 
 
-def build_optimizer(model, base_lr=0.1, nesterov=True, momentum=0.9):
-    return torch.optim.SGD(sgd_param_groups(model, base_lr), lr=base_lr, momentum=momentum,
-                           nesterov=nesterov, foreach=True)
+def merged_param_groups(model: torch.nn.Module, base_lr: float):
+    """The same per-parameter hyper-parameters as :func:`sgd_param_groups`, merged into one
+    group per weight-decay value (3 groups). SGD's update is per parameter, so this is
+    numerically identical, but the multi-tensor (foreach) kernels then cover ~50
+    parameters per launch instead of one: ~660 optimizer launches per step -> ~10."""
+    by_wd = {}
+    for g in sgd_param_groups(model, base_lr):
+        by_wd.setdefault(g["weight_decay"], []).append(g["params"])
+    return [{"params": ps, "lr": base_lr, "weight_decay": wd} for wd, ps in by_wd.items()]
+
+
+def build_optimizer(model, base_lr=0.1, nesterov=True, momentum=0.9, merge_groups=True):
+    groups = (merged_param_groups if merge_groups else sgd_param_groups)(model, base_lr)
+    return torch.optim.SGD(groups, lr=base_lr, momentum=momentum, nesterov=nesterov,
+                           foreach=True)
 
 
 def adjust_learning_rate(optimizer, epoch, base_lr=0.1, steps=(60, 80, 100), warm_up_epoch=0):
