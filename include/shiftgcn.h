@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 1
+#define SGCN_ABI_VERSION 2
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -34,9 +34,11 @@ int sgcn_abi_version(void);
 /* Forward learnable fractional temporal shift.
  * Replaces `shift_cuda.forward(input, xpos, ypos, stride)`
  *   (model/Temporal_shift/cuda/shift_cuda.cpp:19-23 -> shift_cuda_kernel.cu:405-431).
- * in  : (B, C, H, W);  out: (B, C, H/stride, W);  xpos, ypos: (C) raw Shift parameters.
- * The +0.5 that ShiftFunction adds to ypos for stride != 1 (shift.py:17-18) is applied
- * INSIDE the kernel as the same float32 add, so callers pass the raw parameter.
+ * in  : (B, C, H, W);  out: (B, C, H/stride, W);  xpos, ypos: (C) Shift parameters.
+ * ypos_is_raw != 0: ypos is the raw module parameter and the +0.5 that ShiftFunction adds
+ *   for stride != 1 (shift.py:17-18) is applied INSIDE the kernel as the same float32 add
+ *   (the product path: no extra elementwise launch). ypos_is_raw == 0: ypos already holds
+ *   the shifted value, exactly what the reference glue passes to shift_cuda.forward.
  * in_scale/in_shift: optional per-channel affine (C) applied to every in-range input tap
  *   (a fused BatchNorm apply); both NULL = identity.
  * plane_stats: optional (B*C) float2 {mean, M2} of each output plane (n = H/stride*W),
@@ -45,7 +47,7 @@ int sgcn_abi_version(void);
  * once (no memset pass). */
 int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float* ypos,
                     const float* in_scale, const float* in_shift, float* plane_stats,
-                    int B, int C, int H, int W, int stride, void* stream);
+                    int B, int C, int H, int W, int stride, int ypos_is_raw, void* stream);
 
 /* Workspace bytes for sgcn_tshift_bwd (B*C float2 plane partials). */
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
@@ -53,7 +55,8 @@ size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
 /* Backward of the temporal shift. Replaces
  * `shift_cuda.backward(grad_output, input, output, xpos, ypos, stride)`
  *   (shift_cuda.cpp:25-42 -> shift_cuda_kernel.cu:433-523).
- * gout: (B, C, H/stride, W); in: (B, C, H, W) forward input; xpos/ypos raw (see fwd).
+ * gout: (B, C, H/stride, W); in: (B, C, H, W) forward input; xpos/ypos and
+ * ypos_is_raw as in the forward (the reference passes the saved shifted ypos, raw = 0).
  * gin : (B, C, H, W) input gradient (reference Shift_Bottom_Backward*, .cu:78-256);
  * gx, gy: (C) position gradients = mean over batch of the summed position products
  *   (.cu:277-363, 501-509) after applyShiftConstraint (.cu:370-395).
@@ -64,7 +67,7 @@ size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
 int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const float* ypos,
                     const float* in_scale, const float* in_shift, int relu_mask, float* gin,
                     float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
-                    int W, int stride, void* stream);
+                    int W, int stride, int ypos_is_raw, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Pointwise (1x1) channel contraction with the joint-shift gathers fused (fp32 MFMA)

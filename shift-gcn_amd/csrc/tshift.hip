@@ -93,13 +93,13 @@ __global__ __launch_bounds__(kThreads) void tshift_fwd_kernel(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
     const float* __restrict__ ypos, const float* __restrict__ scale,
     const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
-    int Ho, int stride) {
+    int Ho, int stride, int add_half) {
   __shared__ float red[2 * kThreads / 64];
   const int plane = blockIdx.x;
   const int c = plane % C;
   const float* __restrict__ src = in + (size_t)plane * Hb * W;
   float* __restrict__ dst = out + (size_t)plane * Ho * W;
-  const float y = stride == 1 ? ypos[c] : ypos[c] + 0.5f;   // shift.py:17-18 (fp32 add)
+  const float y = add_half ? ypos[c] + 0.5f : ypos[c];   // shift.py:17-18 (fp32 add)
   const Geom g = make_geom(xpos[c], y);
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
@@ -155,7 +155,8 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
     const float* __restrict__ scale, const float* __restrict__ shift,
-    float* __restrict__ gin, float2* __restrict__ pgrad, int C, int Hb, int W, int Ho) {
+    float* __restrict__ gin, float2* __restrict__ pgrad, int C, int Hb, int W, int Ho,
+    int add_half) {
   __shared__ float red[2 * kThreads / 64];
   const int plane = blockIdx.x;
   const int c = plane % C;
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
   const float* __restrict__ src = in + (size_t)plane * Hb * W;
   float* __restrict__ gi = gin + (size_t)plane * Hb * W;
   const float x = xpos[c];
-  const float y = STRIDE == 1 ? ypos[c] : ypos[c] + 0.5f;
+  const float y = add_half ? ypos[c] + 0.5f : ypos[c];
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
 
@@ -277,11 +278,11 @@ __global__ __launch_bounds__(256) void tshift_pos_finalize_kernel(
 template <int EPT>
 void launch_fwd(bool affine, bool stats, const float* in, float* out, const float* xpos,
                 const float* ypos, const float* scale, const float* shift, float2* ps, int B,
-                int C, int H, int W, int Ho, int stride, hipStream_t st) {
+                int C, int H, int W, int Ho, int stride, int add_half, hipStream_t st) {
   dim3 grid(B * C), block(kThreads);
 #define SGCN_FWD(A, S)                                                                     \
   tshift_fwd_kernel<EPT, A, S><<<grid, block, 0, st>>>(in, out, xpos, ypos, scale, shift, \
-                                                      ps, C, H, W, Ho, stride)
+                                                      ps, C, H, W, Ho, stride, add_half)
   if (affine) {
     if (stats) SGCN_FWD(true, true); else SGCN_FWD(true, false);
   } else {
@@ -293,11 +294,12 @@ void launch_fwd(bool affine, bool stats, const float* in, float* out, const floa
 template <int EPT, int STRIDE>
 void launch_bwd(bool affine, bool relu, const float* gout, const float* in, const float* xpos,
                 const float* ypos, const float* scale, const float* shift, float* gin,
-                float2* pg, int B, int C, int H, int W, int Ho, hipStream_t st) {
+                float2* pg, int B, int C, int H, int W, int Ho, int add_half, hipStream_t st) {
   dim3 grid(B * C), block(kThreads);
 #define SGCN_BWD(A, R)                                                                      \
   tshift_bwd_kernel<EPT, A, R, STRIDE><<<grid, block, 0, st>>>(gout, in, xpos, ypos, scale, \
-                                                               shift, gin, pg, C, H, W, Ho)
+                                                               shift, gin, pg, C, H, W, Ho, \
+                                                               add_half)
   if (affine) {
     if (relu) SGCN_BWD(true, true); else SGCN_BWD(true, false);
   } else {
@@ -320,7 +322,7 @@ extern "C" {
 
 int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float* ypos,
                     const float* in_scale, const float* in_shift, float* plane_stats, int B,
-                    int C, int H, int W, int stride, void* stream) {
+                    int C, int H, int W, int stride, int ypos_is_raw, void* stream) {
   SGCN_REQUIRE(B >= 0 && C > 0 && H >= 0 && W > 0 && stride >= 1);
   SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
   const int Ho = H / stride;
@@ -330,10 +332,11 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
   hipStream_t st = (hipStream_t)stream;
   const bool aff = in_scale != nullptr, stats = plane_stats != nullptr;
   float2* ps = (float2*)plane_stats;
+  const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
   switch (pick_ept(Ho * W)) {
-    case 8: launch_fwd<8>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, st); break;
-    case 16: launch_fwd<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, st); break;
-    default: launch_fwd<32>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, st); break;
+    case 8: launch_fwd<8>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
+    case 16: launch_fwd<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
+    default: launch_fwd<32>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
   }
   SGCN_LAUNCH_CHECK();
   return 0;
@@ -344,7 +347,7 @@ size_t sgcn_tshift_bwd_ws_bytes(int B, int C) { return (size_t)B * C * sizeof(fl
 int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const float* ypos,
                     const float* in_scale, const float* in_shift, int relu_mask, float* gin,
                     float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
-                    int W, int stride, void* stream) {
+                    int W, int stride, int ypos_is_raw, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H >= 0 && W > 0 && (stride == 1 || stride == 2));
   SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
   const int Ho = H / stride;
@@ -355,12 +358,13 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   hipStream_t st = (hipStream_t)stream;
   const bool aff = in_scale != nullptr, relu = relu_mask != 0;
   float2* pg = (float2*)ws;
+  const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
   const int ept = pick_ept(H * W);
 #define SGCN_BWD_EPT(E)                                                                     \
   (stride == 1 ? launch_bwd<E, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, gin, \
-                                  pg, B, C, H, W, Ho, st)                                   \
+                                  pg, B, C, H, W, Ho, ah, st)                                   \
                : launch_bwd<E, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, gin, \
-                                  pg, B, C, H, W, Ho, st))
+                                  pg, B, C, H, W, Ho, ah, st))
   if (ept == 8) SGCN_BWD_EPT(8); else if (ept == 16) SGCN_BWD_EPT(16); else SGCN_BWD_EPT(32);
 #undef SGCN_BWD_EPT
   SGCN_LAUNCH_CHECK();

@@ -101,7 +101,8 @@ def _opt(t, name):
 # --------------------------------------------------------------------------------------
 # temporal shift
 # --------------------------------------------------------------------------------------
-def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=None):
+def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=None,
+               ypos_is_raw=True):
     """Forward shift of ``inp`` (B,C,H,W) -> (B,C,H//stride,W). ``ypos`` is the RAW
     parameter (the +0.5 for stride != 1 is applied in-kernel). Optional fused
     per-channel input affine (scale, shift) and per-plane output moments ``stats``
@@ -117,12 +118,14 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
     nb = 4 * (inp.numel() + out.numel())
     with _timed("tshift_fwd", 0, nb, inp):
         rc = lib.sgcn_tshift_fwd(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(scale),
-                                 _ptr(shift), _ptr(stats), B, C, H, W, stride, _stream(inp))
+                                 _ptr(shift), _ptr(stats), B, C, H, W, stride,
+                                 int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_fwd")
     return out
 
 
-def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=False):
+def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=False,
+               ypos_is_raw=True):
     """Backward shift: returns (grad_input, grad_xpos, grad_ypos)."""
     check_input(gout, "grad_output")
     check_input(inp, "input")
@@ -141,7 +144,8 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     with _timed("tshift_bwd", 0, nb, inp):
         rc = lib.sgcn_tshift_bwd(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos), _ptr(scale),
                                  _ptr(shift), int(bool(relu_mask)), _ptr(gin), _ptr(gx),
-                                 _ptr(gy), _ptr(ws), nbytes, B, C, H, W, stride, _stream(inp))
+                                 _ptr(gy), _ptr(ws), nbytes, B, C, H, W, stride,
+                                 int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd")
     return gin, gx, gy
 

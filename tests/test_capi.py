@@ -36,12 +36,12 @@ def test_invalid_arguments_rejected_before_launch():
     from shiftgcn import _lib
     lib = _lib.load()
     # NULL pointers / bad stride / mismatched affine: EINVAL, nothing enqueued
-    assert lib.sgcn_tshift_fwd(None, None, None, None, None, None, None, 2, 3, 4, 5, 1,
+    assert lib.sgcn_tshift_fwd(None, None, None, None, None, None, None, 2, 3, 4, 5, 1, 1,
                                None) == _lib.EINVAL
-    assert lib.sgcn_tshift_fwd(None, None, None, None, None, None, None, 2, 3, 4, 5, 0,
+    assert lib.sgcn_tshift_fwd(None, None, None, None, None, None, None, 2, 3, 4, 5, 0, 1,
                                None) == _lib.EINVAL
     assert lib.sgcn_tshift_bwd(None, None, None, None, None, None, 0, None, None, None, None,
-                               0, 2, 3, 4, 5, 3, None) == _lib.EINVAL
+                               0, 2, 3, 4, 5, 3, 1, None) == _lib.EINVAL
     assert lib.sgcn_tshift_bwd_ws_bytes(4, 8) == 4 * 8 * 8
 
 

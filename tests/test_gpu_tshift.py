@@ -137,3 +137,24 @@ def test_deterministic_position_grads():
     r2 = ops.tshift_bwd(g, x, xpos, ypos, 1)
     for a_, b_ in zip(r1, r2):
         assert torch.equal(a_, b_)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_shift_cuda_compat_module_with_reference_glue_semantics(stride):
+    """shiftgcn.shift_cuda takes the glue's already-shifted ypos (shift.py:17-18)."""
+    from shiftgcn import ShiftFunction, shift_cuda
+    B, C, H, W = 2, 8, 21, 25
+    rng = np.random.default_rng(stride)
+    x = torch.from_numpy(rng.standard_normal((B, C, H, W)).astype(np.float32)).to(DEV)
+    xpos = torch.from_numpy(rng.uniform(-1e-8, 1e-8, C).astype(np.float32)).to(DEV)
+    ypos = torch.from_numpy(rng.uniform(-2, 2, C).astype(np.float32)).to(DEV)
+    ye = ypos if stride == 1 else ypos + 0.5          # what the reference glue passes
+    out = shift_cuda.forward(x, xpos, ye, stride)
+    assert torch.equal(out, ShiftFunction.apply(x, xpos, ypos, stride))
+    g = torch.randn_like(out)
+    gin, gx, gy = shift_cuda.backward(g, x, out, xpos, ye, stride)
+    from shiftgcn import ops
+    r = ops.tshift_bwd(g, x, xpos, ypos, stride)
+    assert torch.equal(gin, r[0]) and torch.equal(gx, r[1]) and torch.equal(gy, r[2])
+    with pytest.raises(RuntimeError, match="must be contiguous"):
+        shift_cuda.forward(x.transpose(2, 3), xpos, ye, stride)
