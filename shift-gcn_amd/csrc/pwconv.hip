@@ -31,6 +31,8 @@ namespace {
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 constexpr int kThreads = 256;
+constexpr int kMaskMaxV = 64;      // joints per row supported by the dW LDS mask table
+constexpr int kMaskFwdMax = 8448;  // V*K floats of the forward LDS mask table (33 x 256)
 
 // A position-mapped plane operand: element (b, ch, n) with n = t*V + v (logical
 // position) lives at ptr[b*bstride + ch*cstride + (t*tstride)*V + rot(v, ch)], where
@@ -67,79 +69,103 @@ __device__ __forceinline__ int pmod(int a, int V) {
   return r < 0 ? r + V : r;
 }
 
+// keep v where ok, exact +0 elsewhere: a bit-AND the compiler cannot turn back into a
+// branch around the (always in-bounds) load
+__device__ __forceinline__ float keep(float v, bool ok) {
+  return __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
+}
+
+// rotation step (d*rsign) mod V in [0, V)
+__device__ __forceinline__ int rot_step(int d, int rsign, int V) { return pmod(d * rsign, V); }
+
 // ------------------------------------------------------------------------------------
 // forward / dX
 // ------------------------------------------------------------------------------------
-template <int BM, int BK, bool MASK, bool RELU, bool ACCUM>
-__global__ __launch_bounds__(kThreads) void pw_fwd_kernel(FwdArgs p) {
+template <int BM, int BK, int WM, bool MASK, bool RELU, bool ACCUM, bool AMC>
+__global__ __launch_bounds__(64 * WM * 2) void pw_fwd_kernel(FwdArgs p) {
+  constexpr int NT = 64 * WM * 2;      // waves: WM along M x 2 along N
   constexpr int BN = 128;
-  constexpr int MI = BM / 64;          // 32-row sub-tiles per wave (waves are 2 x 2)
-  constexpr int NJ = BN / 64;          // 32-col sub-tiles per wave
+  constexpr int MI = BM / WM / 32;     // 32-row sub-tiles per wave
+  constexpr int NJ = BN / 2 / 32;      // 32-col sub-tiles per wave
   constexpr int AP = BM + 1, BP = BN + 1;
-  constexpr int A_PER = BM * BK / kThreads;
-  constexpr int B_PER = BN * BK / kThreads;
+  constexpr int A_PER = BM * BK / NT;
+  constexpr int B_PER = BN * BK / NT;
+  constexpr int KSTEP_B = NT / BN;     // k rows between a thread's B elements
+  static_assert(MI >= 1, "wave tile too small");
   static_assert(A_PER >= 1 && B_PER >= 1, "tile too small");
   __shared__ float As[BK * AP];
   __shared__ float Bs[BK * BP];
-  __shared__ short rot_in[256];
   __shared__ short rot_out[BM];
+  __shared__ float bias_s[BM];
+  __shared__ float mask_s[MASK ? kMaskFwdMax : 1];   // [v][k] feature mask table
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, b = blockIdx.z;
   const int V = p.V, N = p.T * V, K = p.K, M = p.M;
 
-  for (int i = tid; i < K; i += kThreads) rot_in[i] = (short)pmod(p.x.rsign * i, V);
-  for (int i = tid; i < BM; i += kThreads) rot_out[i] = (short)pmod(p.y.rsign * (m0 + i), V);
-  __syncthreads();
+  // row-constant epilogue data staged once (no runtime-conditional load in the epilogue)
+  for (int i = tid; i < BM; i += NT) {
+    rot_out[i] = (short)pmod(p.y.rsign * (m0 + i), V);
+    bias_s[i] = (p.bias && m0 + i < M) ? p.bias[m0 + i] : 0.f;
+  }
+  if (MASK)
+    for (int i = tid; i < V * K; i += NT) mask_s[i] = p.mask[i];
 
-  // B staging: thread owns one column n and rows kb0 + i*(kThreads/BN)
+  // B staging: thread owns column n and rows kb0 + KSTEP_B*i. 32-bit offsets from the
+  // sample's base; the shift_in rotation (v + rsign*k) mod V advances incrementally.
   const int nb = tid % BN, kb0 = tid / BN;
   const int n = n0 + nb;
   const bool nvalid = n < N;
-  const int ncl = min(n, N - 1);           // clamped: loads stay in bounds, value masked
+  const int ncl = min(n, N - 1);
   const int tt = ncl / V;
   const int vv = ncl - tt * V;
-  const float* xb = p.x.ptr + (long long)b * p.x.bstride + (long long)tt * p.x.tstride * V;
+  const float* __restrict__ xb =
+      p.x.ptr + (long long)b * p.x.bstride + (long long)tt * p.x.tstride * V;
+  const int xcs = (int)p.x.cstride;
+  const int bstep = rot_step(KSTEP_B, p.x.rsign, V);
   // A staging
-  const int am = p.a_mcontig ? tid % BM : tid / BK;
-  const int ak = p.a_mcontig ? tid / BM : tid % BK;
-  constexpr int A_MSTEP = kThreads / BK;   // (k-contig) rows per step
-  constexpr int A_KSTEP = kThreads / BM;   // (m-contig) k per step
+  constexpr int A_MSTEP = NT / BK;   // (k-contig) rows per step
+  constexpr int A_KSTEP = NT / BM;   // (m-contig) k per step
+  const int am = AMC ? tid % BM : tid / BK;
+  const int ak = AMC ? tid / BM : tid % BK;
+  const float* __restrict__ A = p.A;
+  const int lda = p.lda;
 
+  // Raw loads only (always in bounds); validity is applied at the LDS store, after the
+  // MFMAs of the current stage, so no instruction consumes a prefetched value early
+  // (consuming it right away made hipcc drain vmcnt(0) after every load).
   float ra[A_PER], rb[B_PER];
   auto load_stage = [&](int k0) {
+    int cv = pmod(vv + p.x.rsign * (k0 + kb0), V);
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int k = k0 + kb0 + i * (kThreads / BN);
-      const int kc = min(k, K - 1);
-      int c = vv + rot_in[kc];
-      c = c >= V ? c - V : c;
-      float v = xb[(long long)kc * p.x.cstride + c];
-      if (MASK) v *= p.mask[vv * K + kc];
-      rb[i] = (nvalid && k < K) ? v : 0.f;
+      const int kc = min(k0 + kb0 + i * KSTEP_B, K - 1);
+      rb[i] = xb[kc * xcs + cv];
+      cv += bstep;
+      cv = cv >= V ? cv - V : cv;
     }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      int m, k;
-      if (p.a_mcontig) { m = am; k = ak + i * A_KSTEP; }
-      else { m = am + i * A_MSTEP; k = ak; }
-      const int gm = m0 + m, gk = k0 + k;
-      const int gmc = min(gm, M - 1), gkc = min(gk, K - 1);
-      const float v = p.a_mcontig ? p.A[(long long)gkc * p.lda + gmc]
-                                  : p.A[(long long)gmc * p.lda + gkc];
-      ra[i] = (gm < M && gk < K) ? v : 0.f;
+      const int m = AMC ? am : am + i * A_MSTEP;
+      const int k = AMC ? ak + i * A_KSTEP : ak;
+      const int gmc = min(m0 + m, M - 1), gkc = min(k0 + k, K - 1);
+      ra[i] = AMC ? A[gkc * lda + gmc] : A[gmc * lda + gkc];
     }
   };
-  auto store_stage = [&]() {
+  auto store_stage = [&](int kst) {
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) Bs[(kb0 + i * (kThreads / BN)) * BP + nb] = rb[i];
+    for (int i = 0; i < B_PER; ++i) {
+      const int k = kst + kb0 + i * KSTEP_B;
+      float v = keep(rb[i], nvalid && k < K);
+      if (MASK) v *= mask_s[vv * K + min(k, K - 1)];
+      Bs[(kb0 + i * KSTEP_B) * BP + nb] = v;
+    }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      int m, k;
-      if (p.a_mcontig) { m = am; k = ak + i * A_KSTEP; }
-      else { m = am + i * A_MSTEP; k = ak; }
-      As[k * AP + m] = ra[i];
+      const int m = AMC ? am : am + i * A_MSTEP;
+      const int k = AMC ? ak + i * A_KSTEP : ak;
+      As[k * AP + m] = keep(ra[i], m0 + m < M && kst + k < K);
     }
   };
 
@@ -152,14 +178,14 @@ __global__ __launch_bounds__(kThreads) void pw_fwd_kernel(FwdArgs p) {
   const int kl = lane >> 5, cl = lane & 31;
   load_stage(0);
   for (int k0 = 0; k0 < K; k0 += BK) {
-    store_stage();
+    store_stage(k0);
     __syncthreads();
     if (k0 + BK < K) load_stage(k0 + BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       float af[MI], bf[NJ];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = As[(kk + kl) * AP + wm * (BM / 2) + i * 32 + cl];
+      for (int i = 0; i < MI; ++i) af[i] = As[(kk + kl) * AP + wm * (BM / WM) + i * 32 + cl];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) bf[j] = Bs[(kk + kl) * BP + wn * (BN / 2) + j * 32 + cl];
 #pragma unroll
@@ -171,28 +197,39 @@ __global__ __launch_bounds__(kThreads) void pw_fwd_kernel(FwdArgs p) {
     __syncthreads();
   }
 
-  // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float* yb = p.y.ptr + (long long)b * p.y.bstride;
+  // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Row-constant data (bias, output rotation) per register; stores are predicated, never
+  // branched around a load (ACCUM loads everything first).
+  float* __restrict__ yb = p.y.ptr + (long long)b * p.y.bstride;
+  const int ycs = (int)p.y.cstride;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = n0 + wn * (BN / 2) + j * 32 + cl;
-    if (col >= N) continue;
-    const int t = col / V, v = col - t * V;
-    float* yt = yb + (long long)t * p.y.tstride * V;
+    const bool cok = col < N;
+    const int colc = min(col, N - 1);
+    const int t = colc / V, v = colc - t * V;
+    const int rowoff = t * p.y.tstride * V;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
+      int off[16];
+      float prev[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        const int m = m0 + row;
-        if (m >= M) continue;
-        float val = acc[i][j][r];
-        if (p.bias) val += p.bias[m];
-        if (RELU) val = fmaxf(val, 0.f);
+        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        const int mc = min(m0 + row, M - 1);
         int vo = v + rot_out[row];
         vo = vo >= V ? vo - V : vo;
-        float* dst = yt + (long long)m * p.y.cstride + vo;
-        if (ACCUM) *dst += val; else *dst = val;
+        off[r] = mc * ycs + rowoff + vo;
+        if (ACCUM) prev[r] = yb[off[r]];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        const int m = m0 + row;
+        float val = acc[i][j][r] + bias_s[row];
+        if (RELU) val = fmaxf(val, 0.f);
+        if (ACCUM) val += prev[r];
+        if (cok && m < M) yb[off[r]] = val;
       }
     }
   }
@@ -211,20 +248,21 @@ struct DwArgs {
   int chunks_per_split;
 };
 
-template <int BM, int BN, bool MASK>
-__global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
+template <int BM, int BN, int WM, int WN, bool MASK>
+__global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
+  constexpr int NT = 64 * WM * WN;
   constexpr int BK = 32;
-  constexpr int MI = BM / 64, NJ = BN / 64;
+  constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
   constexpr int AP = BM + 1, BP = BN + 1;
-  constexpr int RSTEP = kThreads / BK;       // rows per load step (8)
+  constexpr int RSTEP = NT / BK;             // rows per load step
   constexpr int A_PER = BM / RSTEP, B_PER = BN / RSTEP;
+  static_assert(MI >= 1 && NJ >= 1 && A_PER >= 1 && B_PER >= 1, "bad tile");
   __shared__ float As[BK * AP];
   __shared__ float Bs[BK * BP];
-  __shared__ short rot_g[BM];
-  __shared__ short rot_x[BN];
+  __shared__ float mask_s[MASK ? kMaskMaxV * BN : 1];   // [v][c - c0]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int ntiles = (p.Nc + BN - 1) / BN;
   const int m0 = (blockIdx.x / ntiles) * BM, c0 = (blockIdx.x % ntiles) * BN;
   const int split = blockIdx.y;
@@ -234,12 +272,22 @@ __global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
   const int q_end = min(q_begin + p.chunks_per_split, p.B * nchunk);
   const bool want_bias = p.bslab != nullptr && (blockIdx.x % ntiles) == 0;
 
-  for (int i = tid; i < BM; i += kThreads) rot_g[i] = (short)pmod(p.g.rsign * (m0 + i), V);
-  for (int i = tid; i < BN; i += kThreads) rot_x[i] = (short)pmod(p.x.rsign * (c0 + i), V);
-  __syncthreads();
+  if (MASK) {
+    for (int i = tid; i < V * BN; i += NT) {
+      const int v = i / BN, c = c0 + (i - v * BN);
+      mask_s[i] = c < p.Nc ? p.mask[v * p.Nc + c] : 0.f;
+    }
+    __syncthreads();
+  }
 
   const int kq = tid % BK, r0 = tid / BK;
+  // rotation of row r0 + RSTEP*i is (base + i*step) mod V, advanced incrementally
+  const int g_rot0 = pmod(p.g.rsign * (m0 + r0), V), g_step = rot_step(RSTEP, p.g.rsign, V);
+  const int x_rot0 = pmod(p.x.rsign * (c0 + r0), V), x_step = rot_step(RSTEP, p.x.rsign, V);
+  const int gcs = (int)p.g.cstride, xcs = (int)p.x.cstride;
   float ra[A_PER], rb[B_PER], rsum[A_PER];
+  int vcur = 0;
+  bool ncur = false;
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) rsum[i] = 0.f;
 
@@ -250,26 +298,29 @@ __global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
     const int ncl = min(n, N - 1);
     const int t = ncl / V;
     const int v = ncl - t * V;
-    const float* gb = p.g.ptr + (long long)b * p.g.bstride + (long long)t * p.g.tstride * V;
-    const float* xb = p.x.ptr + (long long)b * p.x.bstride + (long long)t * p.x.tstride * V;
+    vcur = v;
+    ncur = nvalid;
+    const float* __restrict__ gb =
+        p.g.ptr + (long long)b * p.g.bstride + (long long)t * p.g.tstride * V;
+    const float* __restrict__ xb =
+        p.x.ptr + (long long)b * p.x.bstride + (long long)t * p.x.tstride * V;
+    int cg = v + g_rot0;
+    cg = cg >= V ? cg - V : cg;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int row = r0 + i * RSTEP, m = m0 + row;
-      const int mc = min(m, p.M - 1);
-      int c = v + rot_g[row];
-      c = c >= V ? c - V : c;
-      const float val = gb[(long long)mc * p.g.cstride + c];
-      ra[i] = (nvalid && m < p.M) ? val : 0.f;
+      const int mc = min(m0 + r0 + i * RSTEP, p.M - 1);
+      ra[i] = gb[mc * gcs + cg];
+      cg += g_step;
+      cg = cg >= V ? cg - V : cg;
     }
+    int cx = v + x_rot0;
+    cx = cx >= V ? cx - V : cx;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int row = r0 + i * RSTEP, c = c0 + row;
-      const int ccl = min(c, p.Nc - 1);
-      int cc = v + rot_x[row];
-      cc = cc >= V ? cc - V : cc;
-      float val = xb[(long long)ccl * p.x.cstride + cc];
-      if (MASK) val *= p.mask[v * p.Nc + ccl];
-      rb[i] = (nvalid && c < p.Nc) ? val : 0.f;
+      const int ccl = min(c0 + r0 + i * RSTEP, p.Nc - 1);
+      rb[i] = xb[ccl * xcs + cx];
+      cx += x_step;
+      cx = cx >= V ? cx - V : cx;
     }
   };
 
@@ -284,20 +335,25 @@ __global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
   for (int q = q_begin; q < q_end; ++q) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      As[kq * AP + r0 + i * RSTEP] = ra[i];
-      rsum[i] += ra[i];
+      const float gv = keep(ra[i], ncur && m0 + r0 + i * RSTEP < p.M);
+      As[kq * AP + r0 + i * RSTEP] = gv;
+      rsum[i] += gv;
     }
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) Bs[kq * BP + r0 + i * RSTEP] = rb[i];
+    for (int i = 0; i < B_PER; ++i) {
+      float xv = keep(rb[i], ncur && c0 + r0 + i * RSTEP < p.Nc);
+      if (MASK) xv *= mask_s[vcur * BN + r0 + i * RSTEP];
+      Bs[kq * BP + r0 + i * RSTEP] = xv;
+    }
     __syncthreads();
     if (q + 1 < q_end) load_stage(q + 1);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       float af[MI], bf[NJ];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = As[(kk + kl) * AP + wm * (BM / 2) + i * 32 + cl];
+      for (int i = 0; i < MI; ++i) af[i] = As[(kk + kl) * AP + wm * (BM / WM) + i * 32 + cl];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bf[j] = Bs[(kk + kl) * BP + wn * (BN / 2) + j * 32 + cl];
+      for (int j = 0; j < NJ; ++j) bf[j] = Bs[(kk + kl) * BP + wn * (BN / WN) + j * 32 + cl];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -310,18 +366,17 @@ __global__ __launch_bounds__(kThreads) void pw_dw_kernel(DwArgs p) {
   float* slab = p.slab + (size_t)split * p.M * p.Nc;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int c = c0 + wn * (BN / 2) + j * 32 + cl;
-    if (c >= p.Nc) continue;
+    const int c = c0 + wn * (BN / WN) + j * 32 + cl;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        if (m < p.M) slab[(size_t)m * p.Nc + c] = acc[i][j][r];
+        const int m = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        if (m < p.M && c < p.Nc) slab[(size_t)m * p.Nc + c] = acc[i][j][r];
       }
   }
   if (want_bias) {
-    // rows r0 + i*RSTEP are shared by the 32 lanes with equal tid/BK (one half-wave)
+    // rows r0 + i*RSTEP are shared by the BK (= 32) lanes with equal tid/BK
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       float s = rsum[i];
@@ -367,10 +422,12 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // ------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------
-template <int BM, int BK>
+template <int BM, int BK, bool AMC>
 void launch_fwd_bm(const FwdArgs& a, int B, bool mask, bool relu, bool accum, hipStream_t st) {
+  constexpr int WM = BM / 32;   // one 32-row sub-tile per wave along M
   dim3 grid((a.M + BM - 1) / BM, (a.T * a.V + 127) / 128, B);
-#define SGCN_PWF(MS, RL, AC) pw_fwd_kernel<BM, BK, MS, RL, AC><<<grid, kThreads, 0, st>>>(a)
+#define SGCN_PWF(MS, RL, AC) \
+  pw_fwd_kernel<BM, BK, WM, MS, RL, AC, AMC><<<grid, 64 * WM * 2, 0, st>>>(a)
   if (mask) {
     if (relu) { if (accum) SGCN_PWF(true, true, true); else SGCN_PWF(true, true, false); }
     else { if (accum) SGCN_PWF(true, false, true); else SGCN_PWF(true, false, false); }
@@ -408,6 +465,8 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   SGCN_REQUIRE(B >= 0 && M > 0 && K > 0 && K <= 256 && T >= 0 && V > 0 && V < 32768);
   SGCN_REQUIRE(x_tstride >= 1 && y_tstride >= 1);
   SGCN_REQUIRE(x_rsign >= -1 && x_rsign <= 1 && y_rsign >= -1 && y_rsign <= 1);
+  SGCN_REQUIRE(x_cstride * (long long)K < (1LL << 31) && y_cstride * (long long)M < (1LL << 31));
+  SGCN_REQUIRE(!mask || V * K <= kMaskFwdMax);
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(w && x && y);
   FwdArgs a;
@@ -424,13 +483,15 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   a.V = V;
   hipStream_t st = (hipStream_t)stream;
   const bool mk = mask != nullptr, rl = relu != 0, ac = accumulate != 0;
+#define SGCN_FWD_BM(BM_, BK_)                                                       \
+  (w_mcontig ? launch_fwd_bm<BM_, BK_, true>(a, B, mk, rl, ac, st)                  \
+             : launch_fwd_bm<BM_, BK_, false>(a, B, mk, rl, ac, st))
   if (K <= 4) {
-    if (M <= 64) launch_fwd_bm<64, 4>(a, B, mk, rl, ac, st);
-    else launch_fwd_bm<128, 4>(a, B, mk, rl, ac, st);
+    if (M <= 64) SGCN_FWD_BM(64, 4); else SGCN_FWD_BM(128, 4);
   } else {
-    if (M <= 64) launch_fwd_bm<64, 32>(a, B, mk, rl, ac, st);
-    else launch_fwd_bm<128, 32>(a, B, mk, rl, ac, st);
+    if (M <= 64) SGCN_FWD_BM(64, 32); else SGCN_FWD_BM(128, 32);
   }
+#undef SGCN_FWD_BM
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -448,7 +509,9 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
                size_t ws_bytes, int B, int M, int Nc, int T, int V, void* stream) {
   SGCN_REQUIRE(B > 0 && M > 0 && Nc > 0 && T > 0 && V > 0 && V < 32768);
   SGCN_REQUIRE(g && x && dw && ws && g_tstride >= 1 && x_tstride >= 1);
+  SGCN_REQUIRE(!mask || V <= kMaskMaxV);
   SGCN_REQUIRE(ws_bytes >= sgcn_pw_dw_ws_bytes(B, M, Nc, T, V));
+  SGCN_REQUIRE(g_cstride * (long long)M < (1LL << 31) && x_cstride * (long long)Nc < (1LL << 31));
   const int bm = dw_tile(M), bn = dw_tile(Nc);
   const int tiles = ((M + bm - 1) / bm) * ((Nc + bn - 1) / bn);
   const int N = T * V;
@@ -468,9 +531,9 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
   a.chunks_per_split = (total + S - 1) / S;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(tiles, S);
-#define SGCN_DW(BM_, BN_)                                                       \
-  (mask ? pw_dw_kernel<BM_, BN_, true><<<grid, kThreads, 0, st>>>(a)           \
-        : pw_dw_kernel<BM_, BN_, false><<<grid, kThreads, 0, st>>>(a))
+#define SGCN_DW(BM_, BN_)                                                           \
+  (mask ? pw_dw_kernel<BM_, BN_, BM_ / 32, 2, true><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a) \
+        : pw_dw_kernel<BM_, BN_, BM_ / 32, 2, false><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a))
   if (bm == 128 && bn == 128) SGCN_DW(128, 128);
   else if (bm == 128) SGCN_DW(128, 64);
   else if (bn == 128) SGCN_DW(64, 128);

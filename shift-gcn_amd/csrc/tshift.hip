@@ -72,18 +72,34 @@ struct Walker {
   }
 };
 
-// Branch-free tap: the load always reads an in-bounds (clamped) address and the value
-// is selected to 0 afterwards, so hipcc never branches around a load (a branch per tap
-// makes it wait vmcnt(0) per element: latency-bound, measured ~1.5 TB/s).
-template <bool AFFINE>
-__device__ __forceinline__ float tap(const float* __restrict__ plane, int r, int c, int H,
-                                     int W, float a, float b) {
-  const bool ok = (unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W;
-  const int rr = min(max(r, 0), H - 1), cc = min(max(c, 0), W - 1);
-  float v = plane[rr * W + cc];
-  if (AFFINE) v = v * a + b;
-  return ok ? v : 0.f;
+// Loads are issued in explicit two-phase sub-chunks of SUB elements per thread: all
+// 4*SUB taps first, then the arithmetic and the stores. Interleaving a store per element
+// (the output may alias the input as far as the compiler knows) serialises every tap
+// load behind a vmcnt wait; batched, 4*SUB loads per thread are in flight.
+constexpr int SUB = 8;
+
+struct TapIdx {
+  int o00, o01, o10, o11;  // clamped in-bounds offsets of the 4 taps
+  float m00, m01, m10, m11;  // 1 where the tap is in range, else 0 (applied as a select)
+};
+
+__device__ __forceinline__ void tap_idx(int r, int c, int H, int W, TapIdx& t) {
+  const bool r0 = (unsigned)r < (unsigned)H, r1 = (unsigned)(r + 1) < (unsigned)H;
+  const bool c0 = (unsigned)c < (unsigned)W, c1 = (unsigned)(c + 1) < (unsigned)W;
+  const int rr0 = min(max(r, 0), H - 1), rr1 = min(max(r + 1, 0), H - 1);
+  const int cc0 = min(max(c, 0), W - 1), cc1 = min(max(c + 1, 0), W - 1);
+  t.o00 = rr0 * W + cc0;
+  t.o01 = rr0 * W + cc1;
+  t.o10 = rr1 * W + cc0;
+  t.o11 = rr1 * W + cc1;
+  t.m00 = (r0 && c0) ? 1.f : 0.f;
+  t.m01 = (r0 && c1) ? 1.f : 0.f;
+  t.m10 = (r1 && c0) ? 1.f : 0.f;
+  t.m11 = (r1 && c1) ? 1.f : 0.f;
 }
+
+// select without a branch: in-range -> v, else exact +0
+__device__ __forceinline__ float sel(float v, float m) { return m != 0.f ? v : 0.f; }
 
 // ------------------------------------------------------------------------------------
 // forward
@@ -110,18 +126,31 @@ __global__ __launch_bounds__(kThreads) void tshift_fwd_kernel(
     float v[EPT];
     Walker pos(base + threadIdx.x, kThreads, W);
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      const int o = base + e * kThreads + threadIdx.x;
-      const int r1 = pos.h * stride + g.y1;
-      const int c1 = pos.w + g.x1;
-      const float q11 = tap<AFFINE>(src, r1, c1, Hb, W, a, b);
-      const float q21 = tap<AFFINE>(src, r1, c1 + 1, Hb, W, a, b);
-      const float q12 = tap<AFFINE>(src, r1 + 1, c1, Hb, W, a, b);
-      const float q22 = tap<AFFINE>(src, r1 + 1, c1 + 1, Hb, W, a, b);
-      const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
-      v[e] = o < n ? val : 0.f;
-      if (o < n) dst[o] = val;
-      pos.next();
+    for (int s0 = 0; s0 < EPT; s0 += SUB) {
+      float q[SUB][4];
+      TapIdx ti[SUB];
+#pragma unroll
+      for (int e = 0; e < SUB; ++e) {
+        tap_idx(pos.h * stride + g.y1, pos.w + g.x1, Hb, W, ti[e]);
+        q[e][0] = src[ti[e].o00];
+        q[e][1] = src[ti[e].o01];
+        q[e][2] = src[ti[e].o10];
+        q[e][3] = src[ti[e].o11];
+        pos.next();
+      }
+#pragma unroll
+      for (int e = 0; e < SUB; ++e) {
+        float q11 = q[e][0], q21 = q[e][1], q12 = q[e][2], q22 = q[e][3];
+        if (AFFINE) { q11 = q11 * a + b; q21 = q21 * a + b; q12 = q12 * a + b; q22 = q22 * a + b; }
+        q11 = sel(q11, ti[e].m00);
+        q21 = sel(q21, ti[e].m01);
+        q12 = sel(q12, ti[e].m10);
+        q22 = sel(q22, ti[e].m11);
+        const int o = base + (s0 + e) * kThreads + threadIdx.x;
+        const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
+        v[s0 + e] = o < n ? val : 0.f;
+        if (o < n) dst[o] = val;
+      }
     }
     if (STATS) {
       const int cnt = min(n - base, EPT * kThreads);
@@ -178,31 +207,43 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
     for (int base = 0; base < nb; base += EPT * kThreads) {
       Walker pos(base + threadIdx.x, kThreads, W);
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        const int o = base + e * kThreads + threadIdx.x;
-        const int h1 = pos.h + r.y1, h2 = h1 + 1;
-        const int w1 = pos.w + r.x1, w2 = w1 + 1;
-        float q11, q21, q12, q22;
-        if (STRIDE == 1) {
-          q11 = tap<false>(go, h1, w1, Ho, W, 1.f, 0.f);
-          q21 = tap<false>(go, h1, w2, Ho, W, 1.f, 0.f);
-          q12 = tap<false>(go, h2, w1, Ho, W, 1.f, 0.f);
-          q22 = tap<false>(go, h2, w2, Ho, W, 1.f, 0.f);
-        } else {
-          // h_im % 2 == 0 (C++ remainder), then h_im / 2 (truncation), bounds on top grid;
-          // odd h_im -> row index -1 (rejected by the bounds test)
-          const int hq1 = (h1 % 2 == 0) ? h1 / 2 : -1;
-          const int hq2 = (h2 % 2 == 0) ? h2 / 2 : -1;
-          q11 = tap<false>(go, hq1, w1, Ho, W, 1.f, 0.f);
-          q21 = tap<false>(go, hq1, w2, Ho, W, 1.f, 0.f);
-          q12 = tap<false>(go, hq2, w1, Ho, W, 1.f, 0.f);
-          q22 = tap<false>(go, hq2, w2, Ho, W, 1.f, 0.f);
+      for (int s0 = 0; s0 < EPT; s0 += SUB) {
+        float q[SUB][4], rin[SUB];
+        TapIdx ti[SUB];
+#pragma unroll
+        for (int e = 0; e < SUB; ++e) {
+          const int h1 = pos.h + r.y1;
+          const int w1 = pos.w + r.x1;
+          if (STRIDE == 1) {
+            tap_idx(h1, w1, Ho, W, ti[e]);
+          } else {
+            // h_im % 2 == 0 (C++ remainder), then h_im / 2 (truncation), bounds on the top
+            // grid; exactly one of h1, h1+1 is even
+            const int h2 = h1 + 1;
+            const int hq1 = (h1 % 2 == 0) ? h1 / 2 : -1;
+            const int hq2 = (h2 % 2 == 0) ? h2 / 2 : -1;
+            TapIdx t1, t2;
+            tap_idx(hq1, w1, Ho, W, t1);
+            tap_idx(hq2, w1, Ho, W, t2);
+            ti[e].o00 = t1.o00; ti[e].o01 = t1.o01; ti[e].m00 = t1.m00; ti[e].m01 = t1.m01;
+            ti[e].o10 = t2.o00; ti[e].o11 = t2.o01; ti[e].m10 = t2.m00; ti[e].m11 = t2.m01;
+          }
+          q[e][0] = go[ti[e].o00];
+          q[e][1] = go[ti[e].o01];
+          q[e][2] = go[ti[e].o10];
+          q[e][3] = go[ti[e].o11];
+          if (RELU_MASK) rin[e] = src[min(base + (s0 + e) * kThreads + (int)threadIdx.x, nb - 1)];
+          pos.next();
         }
-        float val = blend(q11, q21, q12, q22, r.dx, r.dy);
-        const int oc = min(o, nb - 1);
-        if (RELU_MASK) val = src[oc] > 0.f ? val : 0.f;
-        if (o < nb) gi[o] = val;
-        pos.next();
+#pragma unroll
+        for (int e = 0; e < SUB; ++e) {
+          const float q11 = sel(q[e][0], ti[e].m00), q21 = sel(q[e][1], ti[e].m01);
+          const float q12 = sel(q[e][2], ti[e].m10), q22 = sel(q[e][3], ti[e].m11);
+          float val = blend(q11, q21, q12, q22, r.dx, r.dy);
+          if (RELU_MASK) val = rin[e] > 0.f ? val : 0.f;
+          const int o = base + (s0 + e) * kThreads + threadIdx.x;
+          if (o < nb) gi[o] = val;
+        }
       }
     }
   }
@@ -215,20 +256,34 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
     for (int base = 0; base < nt; base += EPT * kThreads) {
       Walker pos(base + threadIdx.x, kThreads, W);
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        const int o = base + e * kThreads + threadIdx.x;
-        const int r1 = pos.h * STRIDE + g.y1;
-        const int c1 = pos.w + g.x1;
-        const float q11 = tap<AFFINE>(src, r1, c1, Hb, W, a, b);
-        const float q21 = tap<AFFINE>(src, r1, c1 + 1, Hb, W, a, b);
-        const float q12 = tap<AFFINE>(src, r1 + 1, c1, Hb, W, a, b);
-        const float q22 = tap<AFFINE>(src, r1 + 1, c1 + 1, Hb, W, a, b);
-        const float vx = (1.f - g.dy) * (q21 - q11) + g.dy * (q22 - q12);
-        const float vy = (1.f - g.dx) * (q12 - q11) + g.dx * (q22 - q21);
-        const float gv = o < nt ? go[min(o, nt - 1)] : 0.f;
-        ax += vx * gv;
-        ay += vy * gv;
-        pos.next();
+      for (int s0 = 0; s0 < EPT; s0 += SUB) {
+        float q[SUB][4], gv[SUB];
+        TapIdx ti[SUB];
+#pragma unroll
+        for (int e = 0; e < SUB; ++e) {
+          tap_idx(pos.h * STRIDE + g.y1, pos.w + g.x1, Hb, W, ti[e]);
+          q[e][0] = src[ti[e].o00];
+          q[e][1] = src[ti[e].o01];
+          q[e][2] = src[ti[e].o10];
+          q[e][3] = src[ti[e].o11];
+          gv[e] = go[min(base + (s0 + e) * kThreads + (int)threadIdx.x, nt - 1)];
+          pos.next();
+        }
+#pragma unroll
+        for (int e = 0; e < SUB; ++e) {
+          float q11 = q[e][0], q21 = q[e][1], q12 = q[e][2], q22 = q[e][3];
+          if (AFFINE) { q11 = q11 * a + b; q21 = q21 * a + b; q12 = q12 * a + b; q22 = q22 * a + b; }
+          q11 = sel(q11, ti[e].m00);
+          q21 = sel(q21, ti[e].m01);
+          q12 = sel(q12, ti[e].m10);
+          q22 = sel(q22, ti[e].m11);
+          const float vx = (1.f - g.dy) * (q21 - q11) + g.dy * (q22 - q12);
+          const float vy = (1.f - g.dx) * (q12 - q11) + g.dx * (q22 - q21);
+          const int o = base + (s0 + e) * kThreads + threadIdx.x;
+          const float gg = o < nt ? gv[e] : 0.f;
+          ax += vx * gg;
+          ay += vy * gg;
+        }
       }
     }
   }
