@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 2
+#define SGCN_ABI_VERSION 3
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -132,10 +132,12 @@ int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
                       float* scale, float* shift, void* stream);
 
 /* y = act(x*scale[f] + shift[f] + res), res = r*rscale[c] + rshift[c] (both given),
- * r (rscale NULL) or 0 (r NULL); act = ReLU if relu. */
+ * r (rscale NULL) or 0 (r NULL); act = ReLU if relu. y_stats (optional, B*C float2):
+ * per-plane {mean, M2} of y, i.e. the sgcn_moments() partials of the NEXT BatchNorm2d's
+ * input, produced without another read of y. */
 int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
                   const float* r, const float* rscale, const float* rshift, int relu,
-                  float* y, int B, int C, int T, int V, void* stream);
+                  float* y, float* y_stats, int B, int C, int T, int V, void* stream);
 
 /* Backward partials: g = dy * (relu ? y > 0 : 1); part[b][f] = {sum g, sum g*xhat};
  * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none). */

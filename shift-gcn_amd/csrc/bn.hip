@@ -173,12 +173,15 @@ __global__ void bn_eval_coef_kernel(int F, int perm_V, const float* __restrict__
 // ------------------------------------------------------------------------------------
 // apply: y = act(x*scale[f] + shift[f] + res); res = r*rscale[c] + rshift[c] | r | 0
 // ------------------------------------------------------------------------------------
-template <bool PER_JOINT, int RES, bool RELU>
+// OUT_STATS: also write the per-plane {mean, M2} of y (moments of the NEXT BatchNorm's
+// input, shifted by the plane's first output), saving a separate read pass of y.
+template <bool PER_JOINT, int RES, bool RELU, bool OUT_STATS>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     const float* __restrict__ x, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ r,
     const float* __restrict__ rscale, const float* __restrict__ rshift,
-    float* __restrict__ y, int C, int T, int V) {
+    float* __restrict__ y, float2* __restrict__ ystats, int C, int T, int V) {
+  __shared__ float red[2 * kThreads / 64];
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
   const size_t off = (size_t)plane * P;
@@ -187,6 +190,16 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
   if (RES == 2) { rsc = rscale[c]; rsh = rshift[c]; }
   const int dv = kThreads % V;
   int v = threadIdx.x % V;
+  float k0 = 0.f, s1 = 0.f, s2 = 0.f;
+  if (OUT_STATS) {  // shift = the plane's first output value (same formula, element 0)
+    float a = x[off];
+    if (PER_JOINT) a = a * scale[c * V] + shift[c * V];
+    else a = a * sc + sh;
+    if (RES == 1) a += r[off];
+    if (RES == 2) a += r[off] * rsc + rsh;
+    if (RELU) a = fmaxf(a, 0.f);
+    k0 = a;
+  }
   for (int base = 0; base < P; base += kThreads * kU) {
     float xv[kU], rv[kU];
 #pragma unroll
@@ -205,8 +218,20 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
       if (RES == 2) a += rv[u] * rsc + rsh;
       if (RELU) a = fmaxf(a, 0.f);
       if (o < P) y[off + o] = a;
+      if (OUT_STATS) {
+        const float d = o < P ? a - k0 : 0.f;
+        s1 += d;
+        s2 += d * d;
+      }
       v += dv;
       if (v >= V) v -= V;
+    }
+  }
+  if (OUT_STATS) {
+    block_sum2(s1, s2, red);
+    if (threadIdx.x == 0) {
+      const float n = (float)P;
+      ystats[plane] = make_float2(k0 + s1 / n, s2 - s1 * s1 / n);
     }
   }
 }
@@ -522,7 +547,7 @@ int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
 
 int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
                   const float* r, const float* rscale, const float* rshift, int relu,
-                  float* y, int B, int C, int T, int V, void* stream) {
+                  float* y, float* y_stats, int B, int C, int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(x && scale && shift && y);
@@ -530,8 +555,12 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
   hipStream_t st = (hipStream_t)stream;
   const int res = r == nullptr ? 0 : (rscale ? 2 : 1);
   dim3 g(B * C);
-#define SGCN_APPLY(PJ, RS, RL) \
-  bn_apply_kernel<PJ, RS, RL><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale, rshift, y, C, T, V)
+  float2* ys = (float2*)y_stats;
+#define SGCN_APPLY(PJ, RS, RL)                                                                    \
+  (ys ? bn_apply_kernel<PJ, RS, RL, true><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale,     \
+                                                                  rshift, y, ys, C, T, V)         \
+      : bn_apply_kernel<PJ, RS, RL, false><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale,    \
+                                                                   rshift, y, ys, C, T, V))
 #define SGCN_APPLY_R(PJ, RL) \
   if (res == 0) SGCN_APPLY(PJ, 0, RL); else if (res == 1) SGCN_APPLY(PJ, 1, RL); else SGCN_APPLY(PJ, 2, RL)
   if (per_joint) { if (relu) { SGCN_APPLY_R(true, true); } else { SGCN_APPLY_R(true, false); } }

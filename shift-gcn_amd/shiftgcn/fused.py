@@ -40,7 +40,7 @@ def _empty(*shape, like):
 # Shift_gcn
 # ======================================================================================
 class GcnSaved:
-    __slots__ = ("x0", "Z", "zst", "D0", "dst", "H", "m")
+    __slots__ = ("x0", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
 
 
 def gcn_forward(mod, x0, training):
@@ -63,11 +63,12 @@ def gcn_forward(mod, x0, training):
             dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn)
         else:
             dst = ops.bn_eval_coef(bn, Cout)
-        H = ops.bn_apply(Z, zst, True, r=D0, rst=dst, relu=True)
+        H, hm = ops.bn_apply(Z, zst, True, r=D0, rst=dst, relu=True, out_stats=training)
     else:
-        H = ops.bn_apply(Z, zst, True, r=x0, relu=True)
+        H, hm = ops.bn_apply(Z, zst, True, r=x0, relu=True, out_stats=training)
     s = GcnSaved()
     s.x0, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, Z, zst, D0, dst, H, m
+    s.h_moments = hm   # moments of H for Shift_tcn.bn, produced by the same launch
     return H, s
 
 
@@ -120,15 +121,18 @@ class TcnSaved:
     __slots__ = ("H", "ast", "As", "R", "S", "sst")
 
 
-def tcn_core_forward(mod, H, training):
+def tcn_core_forward(mod, H, training, h_moments=None):
     """bn -> shift_in -> temporal_linear -> ReLU -> shift_out; returns (S, bn2 stats, saved)
-    where S is the shift_out output BEFORE bn2."""
+    where S is the shift_out output BEFORE bn2. ``h_moments``: per-plane moments of H
+    already produced by the launch that wrote H (else computed here)."""
     B, C, T, V = H.shape
     Cout = mod.out_channels
     si, so = mod.shift_in, mod.shift_out
     stride = so.stride
     if training:
-        ast = ops.bn_finalize(ops.moments(H, False), B, C, T * V, mod.bn)
+        if h_moments is None:
+            h_moments = ops.moments(H, False)
+        ast = ops.bn_finalize(h_moments, B, C, T * V, mod.bn)
     else:
         ast = ops.bn_eval_coef(mod.bn, C)
     As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=ast.scale,
@@ -220,7 +224,7 @@ class UnitSaved:
 
 def unit_forward(unit, x, training):
     H, gs = gcn_forward(unit.gcn1, x, training)
-    S, sst, ts = tcn_core_forward(unit.tcn1, H, training)
+    S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
     rs = None
     if unit.residual_kind == "conv":
         Rc, rst, rs = convbn_core_forward(unit.residual, x, training)

@@ -252,18 +252,21 @@ def bn_eval_coef(bn, F, perm_V=0, device=None):
     return st
 
 
-def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False, out=None):
+def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False, out=None,
+             out_stats=False):
+    """Returns y, or (y, per-plane moments of y) with ``out_stats``."""
     check_input(x, "input")
     if r is not None:
         check_input(r, "residual")
     B, C, T, V = x.shape
     y = torch.empty_like(x) if out is None else out
+    ys = torch.empty((B * C * 2,), device=x.device, dtype=_F32) if out_stats else None
     rc = _lib.load().sgcn_bn_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift), int(per_joint),
                                    _ptr(r), _ptr(rst.scale) if rst else None,
-                                   _ptr(rst.shift) if rst else None, int(relu), _ptr(y), B, C,
-                                   T, V, _stream(x))
+                                   _ptr(rst.shift) if rst else None, int(relu), _ptr(y),
+                                   _ptr(ys), B, C, T, V, _stream(x))
     _lib.check(rc, "sgcn_bn_apply")
-    return y
+    return (y, ys) if out_stats else y
 
 
 def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats = None):
