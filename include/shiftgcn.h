@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 3
+#define SGCN_ABI_VERSION 4
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -126,10 +126,11 @@ int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
                      float* running_mean, float* running_var, long long* num_batches,
                      float* mean, float* invstd, float* scale, float* shift, void* stream);
 
-/* Eval-mode scale/shift from running statistics. */
+/* Eval-mode coefficients from running statistics: scale/shift (and, when non-NULL, the
+ * running mean and 1/sqrt(running_var + eps) used by an eval-mode backward). */
 int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
                       const float* running_mean, const float* running_var, float eps,
-                      float* scale, float* shift, void* stream);
+                      float* mean, float* invstd, float* scale, float* shift, void* stream);
 
 /* y = act(x*scale[f] + shift[f] + res), res = r*rscale[c] + rshift[c] (both given),
  * r (rscale NULL) or 0 (r NULL); act = ReLU if relu. y_stats (optional, B*C float2):
@@ -147,11 +148,12 @@ int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x
                        int B, int C, int T, int V, void* stream);
 
 /* dgamma/dbeta (+)= sums (reference feature order); coef[3][F] = {k1, k2, k3} such that
- * dx = k1*g + k2*x + k3 (training-mode BatchNorm input gradient). */
+ * dx = k1*g + k2*x + k3: the training-mode BatchNorm input gradient (batch_stats = 1), or
+ * the eval-mode one (batch_stats = 0: k2 = k3 = 0, mean/invstd = running statistics). */
 int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int perm_V,
                          const float* mean, const float* invstd, const float* gamma,
-                         float* dgamma, float* dbeta, int accumulate, float* coef,
-                         void* stream);
+                         float* dgamma, float* dbeta, int accumulate, int batch_stats,
+                         float* coef, void* stream);
 
 /* dx = k1*g + k2*x + k3; dr = g (rcoef NULL, dr given) or rk1*g + rk2*r + rk3. */
 int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,

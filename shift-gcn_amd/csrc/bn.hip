@@ -159,6 +159,8 @@ __global__ void bn_eval_coef_kernel(int F, int perm_V, const float* __restrict__
                                     const float* __restrict__ beta,
                                     const float* __restrict__ running_mean,
                                     const float* __restrict__ running_var, float eps,
+                                    float* __restrict__ mean_out,
+                                    float* __restrict__ invstd_out,
                                     float* __restrict__ scale_out,
                                     float* __restrict__ shift_out) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -166,6 +168,8 @@ __global__ void bn_eval_coef_kernel(int F, int perm_V, const float* __restrict__
   const int rf = ref_feature(f, perm_V, F);
   const float invstd = (float)(1.0 / sqrt((double)running_var[rf] + (double)eps));
   const float scale = (gamma ? gamma[rf] : 1.f) * invstd;
+  if (mean_out) mean_out[f] = running_mean[rf];
+  if (invstd_out) invstd_out[f] = invstd;
   scale_out[f] = scale;
   shift_out[f] = (beta ? beta[rf] : 0.f) - running_mean[rf] * scale;
 }
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
     const float2* __restrict__ part, int B, int F, double n_total, int perm_V,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    int accumulate, float* __restrict__ coef) {
+    int accumulate, int batch_stats, float* __restrict__ coef) {
   double sg, sgx, unused;
   int f;
   if (!feature_sums(part, B, F, sg, sgx, unused, f)) return;
@@ -336,8 +340,10 @@ __global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
   const float g = gamma ? gamma[rf] : 1.f;
   const float is = invstd[f];
   const float k1 = g * is;
-  const float k2 = (float)(-(double)k1 * (double)is * (sgx / n_total));
-  const float k3 = (float)(-(double)k1 * (sg / n_total) - (double)k2 * (double)mean[f]);
+  // running-statistics (eval) BatchNorm is a fixed affine map: dx = k1 * g
+  const float k2 = batch_stats ? (float)(-(double)k1 * (double)is * (sgx / n_total)) : 0.f;
+  const float k3 = batch_stats ? (float)(-(double)k1 * (sg / n_total) - (double)k2 * (double)mean[f])
+                               : 0.f;
   coef[f] = k1;
   coef[F + f] = k2;
   coef[2 * F + f] = k3;
@@ -536,11 +542,11 @@ int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
 
 int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
                       const float* running_mean, const float* running_var, float eps,
-                      float* scale, float* shift, void* stream) {
+                      float* mean, float* invstd, float* scale, float* shift, void* stream) {
   SGCN_REQUIRE(F > 0 && running_mean && running_var && scale && shift);
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
   bn_eval_coef_kernel<<<(F + 255) / 256, 256, 0, (hipStream_t)stream>>>(
-      F, perm_V, gamma, beta, running_mean, running_var, eps, scale, shift);
+      F, perm_V, gamma, beta, running_mean, running_var, eps, mean, invstd, scale, shift);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -599,13 +605,13 @@ int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x
 
 int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int perm_V,
                          const float* mean, const float* invstd, const float* gamma,
-                         float* dgamma, float* dbeta, int accumulate, float* coef,
-                         void* stream) {
+                         float* dgamma, float* dbeta, int accumulate, int batch_stats,
+                         float* coef, void* stream) {
   SGCN_REQUIRE(part && B > 0 && F > 0 && n_total > 0 && mean && invstd && coef);
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
   bn_bwd_finalize_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSlices, 0, (hipStream_t)stream>>>(
       (const float2*)part, B, F, (double)n_total, perm_V, mean, invstd, gamma, dgamma, dbeta,
-      accumulate, coef);
+      accumulate, batch_stats, coef);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

@@ -289,8 +289,6 @@ class _BlockFunction(torch.autograd.Function):
     def forward(ctx, impl, module, x, *params):
         fwd, bwd = impl
         training = module.training
-        if not training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
-            pass  # eval-mode forward; backward below refuses (BN in eval has no batch stats)
         y, saved = fwd(module, x.contiguous(), training)
         ctx.impl, ctx.module, ctx.saved, ctx.training = impl, module, saved, training
         ctx.names = [n for n, _ in trainable(module)]
@@ -298,10 +296,8 @@ class _BlockFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        if not ctx.training:
-            raise NotImplementedError(
-                "backward through an eval-mode (running-stats) Shift-GCN block is not "
-                "supported by the HIP path; call .train() for training")
+        # eval-mode blocks back-propagate through their running-statistics BatchNorms
+        # (fixed affine maps); the BnStats objects saved by the forward carry the mode
         _, bwd = ctx.impl
         dx, grads = bwd(ctx.module, ctx.saved, dy.contiguous())
         ctx.saved = None

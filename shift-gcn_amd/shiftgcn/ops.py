@@ -216,13 +216,15 @@ def moments(x, per_joint):
 
 
 class BnStats:
-    """Batch statistics and apply coefficients of one BatchNorm call (local feature order)."""
+    """Statistics and apply coefficients of one BatchNorm call (local feature order):
+    batch statistics in training mode, running statistics in eval mode (``batch``)."""
 
-    __slots__ = ("mean", "invstd", "scale", "shift")
+    __slots__ = ("mean", "invstd", "scale", "shift", "batch")
 
-    def __init__(self, F, device):
+    def __init__(self, F, device, batch=True):
         buf = torch.empty((4, F), device=device, dtype=_F32)
         self.mean, self.invstd, self.scale, self.shift = buf[0], buf[1], buf[2], buf[3]
+        self.batch = batch
 
 
 def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
@@ -243,10 +245,11 @@ def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
 
 
 def bn_eval_coef(bn, F, perm_V=0, device=None):
-    st = BnStats(F, bn.running_mean.device)
+    st = BnStats(F, bn.running_mean.device, batch=False)
     rc = _lib.load().sgcn_bn_eval_coef(F, perm_V, _ptr(bn.weight), _ptr(bn.bias),
                                        _ptr(bn.running_mean), _ptr(bn.running_var),
-                                       float(bn.eps), _ptr(st.scale), _ptr(st.shift),
+                                       float(bn.eps), _ptr(st.mean), _ptr(st.invstd),
+                                       _ptr(st.scale), _ptr(st.shift),
                                        _stream(bn.running_mean))
     _lib.check(rc, "sgcn_bn_eval_coef")
     return st
@@ -292,8 +295,8 @@ def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
     dbeta = torch.empty_like(bn.bias) if bn.bias is not None else None
     rc = _lib.load().sgcn_bn_bwd_finalize(_ptr(part), B, F, int(n_total), perm_V,
                                           _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
-                                          _ptr(dgamma), _ptr(dbeta), 0, _ptr(coef),
-                                          _stream(part))
+                                          _ptr(dgamma), _ptr(dbeta), 0, int(st.batch),
+                                          _ptr(coef), _stream(part))
     _lib.check(rc, "sgcn_bn_bwd_finalize")
     return coef, dgamma, dbeta
 

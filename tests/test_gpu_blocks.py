@@ -212,3 +212,18 @@ def test_model_matches_golden_fixture(golden, case):
             flips_ours += int((np.sign(params[n].grad.cpu().numpy()) != s64).sum())
             flips_ref += int((np.sign(fx[f"model_{name}_grad.{n}"]) != s64).sum())
     assert flips_ours <= 2 * flips_ref + 2, (flips_ours, flips_ref)
+
+
+@pytest.mark.parametrize("kind,cin,cout,stride", [("unit", 64, 128, 2), ("unit", 64, 64, 1),
+                                                  ("gcn", 3, 64, 1), ("tcn", 64, 64, 2)])
+def test_eval_mode_backward_matches_oracle(kind, cin, cout, stride):
+    """Backward through running-statistics BatchNorms (e.g. fine-tuning with frozen BN)."""
+    ref, ours = _pair(kind, cin, cout, 25, stride, seed=5 + cin + cout)
+    ref.eval()
+    ours.eval()
+    T = 12
+    x = formula.tensor((2, cin, T, 25), 8 + cin, 1.0)
+    To = T // stride if kind != "gcn" else T
+    g = formula.tensor((2, cout, To, 25), 9 + cout, 1.0)
+    xr, yr, xo, yo = _run_pair(ref, ours, x, g)
+    _compare(ref, ours, xr, yr, xo, yo, f"eval-{kind}")
