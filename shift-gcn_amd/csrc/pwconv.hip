@@ -111,6 +111,7 @@ __global__ __launch_bounds__(64 * WM * 2) void pw_fwd_kernel(FwdArgs p) {
   }
   if (MASK)
     for (int i = tid; i < V * K; i += NT) mask_s[i] = p.mask[i];
+  __syncthreads();   // rot_out / bias_s / mask_s are read before the main loop's barrier
 
   // B staging: thread owns column n and rows kb0 + KSTEP_B*i. 32-bit offsets from the
   // sample's base; the shift_in rotation (v + rsign*k) mod V advances incrementally.

@@ -256,8 +256,8 @@ def bn_eval_coef(bn, F, perm_V=0, device=None):
 
 
 def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False, out=None,
-             out_stats=False):
-    """Returns y, or (y, per-plane moments of y) with ``out_stats``."""
+             out_stats=None):
+    """Returns y; with ``out_stats`` given (True/False) returns (y, moments of y or None)."""
     check_input(x, "input")
     if r is not None:
         check_input(r, "residual")
@@ -269,7 +269,7 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
                                    _ptr(rst.shift) if rst else None, int(relu), _ptr(y),
                                    _ptr(ys), B, C, T, V, _stream(x))
     _lib.check(rc, "sgcn_bn_apply")
-    return (y, ys) if out_stats else y
+    return y if out_stats is None else (y, ys)
 
 
 def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats = None):
