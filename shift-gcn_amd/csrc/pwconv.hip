@@ -182,18 +182,33 @@ __global__ __launch_bounds__(64 * WM * 2) void pw_fwd_kernel(FwdArgs p) {
     store_stage(k0);
     __syncthreads();
     if (k0 + BK < K) load_stage(k0 + BK);
+    // fragments double-buffered in registers: the LDS reads of k-step kk+2 are in
+    // flight while the MFMAs of k-step kk issue (no lgkmcnt(0) stall per k-step)
+    float af[2][MI], bf[2][NJ];
+    const float* __restrict__ Aw = As + kl * AP + wm * (BM / WM) + cl;
+    const float* __restrict__ Bw = Bs + kl * BP + wn * (BN / 2) + cl;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[0][i] = Aw[i * 32];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[0][j] = Bw[j * 32];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      float af[MI], bf[NJ];
+      const int cur = (kk >> 1) & 1;
+      if (kk + 2 < BK) {
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = As[(kk + kl) * AP + wm * (BM / WM) + i * 32 + cl];
+        for (int i = 0; i < MI; ++i) af[cur ^ 1][i] = Aw[(kk + 2) * AP + i * 32];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bf[j] = Bs[(kk + kl) * BP + wn * (BN / 2) + j * 32 + cl];
+        for (int j = 0; j < NJ; ++j) bf[cur ^ 1][j] = Bw[(kk + 2) * BP + j * 32];
+      }
+      // keep the prefetch reads above this k-step's MFMAs (the scheduler otherwise sinks
+      // them below to reuse registers, exposing LDS latency every k-step)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][i], bf[cur][j], acc[i][j],
+                                                           0, 0, 0);
     }
     __syncthreads();
   }
@@ -348,18 +363,31 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
     }
     __syncthreads();
     if (q + 1 < q_end) load_stage(q + 1);
+    float af[2][MI], bf[2][NJ];
+    const float* __restrict__ Aw = As + kl * AP + wm * (BM / WM) + cl;
+    const float* __restrict__ Bw = Bs + kl * BP + wn * (BN / WN) + cl;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[0][i] = Aw[i * 32];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[0][j] = Bw[j * 32];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      float af[MI], bf[NJ];
+      const int cur = (kk >> 1) & 1;
+      if (kk + 2 < BK) {
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = As[(kk + kl) * AP + wm * (BM / WM) + i * 32 + cl];
+        for (int i = 0; i < MI; ++i) af[cur ^ 1][i] = Aw[(kk + 2) * AP + i * 32];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bf[j] = Bs[(kk + kl) * BP + wn * (BN / WN) + j * 32 + cl];
+        for (int j = 0; j < NJ; ++j) bf[cur ^ 1][j] = Bw[(kk + 2) * BP + j * 32];
+      }
+      // keep the prefetch reads above this k-step's MFMAs (the scheduler otherwise sinks
+      // them below to reuse registers, exposing LDS latency every k-step)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][i], bf[cur][j], acc[i][j],
+                                                           0, 0, 0);
     }
     __syncthreads();
   }
