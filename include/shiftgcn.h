@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 4
+#define SGCN_ABI_VERSION 5
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -63,9 +63,14 @@ size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
  * in_scale/in_shift: same optional affine as the forward (the position products then
  *   use the affine taps). relu_mask != 0: gin[p] = 0 where in[p] <= 0 (fused ReLU
  *   backward for a shift whose input is a ReLU output).
+ * bn_mean/bn_invstd/bn_part (optional, all or none): also write bn_part[b*C+c] =
+ *   {sum gin, sum gin*(in - bn_mean[c])*bn_invstd[c]} over the plane — the
+ *   sgcn_bn_bwd_reduce() partials of the BatchNorm whose output feeds this shift
+ *   (Shift_tcn.bn -> shift_in), without another pass over gin and in.
  * stride must be 1 or 2 (the reference backward hard-codes 2 for stride != 1). */
 int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const float* ypos,
-                    const float* in_scale, const float* in_shift, int relu_mask, float* gin,
+                    const float* in_scale, const float* in_shift, int relu_mask,
+                    const float* bn_mean, const float* bn_invstd, float* bn_part, float* gin,
                     float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                     int W, int stride, int ypos_is_raw, void* stream);
 
@@ -141,11 +146,14 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
                   float* y, float* y_stats, int B, int C, int T, int V, void* stream);
 
 /* Backward partials: g = dy * (relu ? y > 0 : 1); part[b][f] = {sum g, sum g*xhat};
- * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none). */
+ * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none).
+ * dy_coef (optional, [3][C], requires relu): dy is replaced by k1[c]*dy + k2[c]*y + k3[c],
+ * i.e. the input gradient of the following BatchNorm2d (whose input is y), computed on the
+ * fly instead of materialised (Shift_tcn.bn's dx feeding Shift_gcn's ReLU/BN backward). */
 int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x,
                        const float* mean, const float* invstd, int per_joint, const float* r,
-                       const float* rmean, const float* rinvstd, float* part, float* rpart,
-                       int B, int C, int T, int V, void* stream);
+                       const float* rmean, const float* rinvstd, const float* dy_coef,
+                       float* part, float* rpart, int B, int C, int T, int V, void* stream);
 
 /* dgamma/dbeta (+)= sums (reference feature order); coef[3][F] = {k1, k2, k3} such that
  * dx = k1*g + k2*x + k3: the training-mode BatchNorm input gradient (batch_stats = 1), or
@@ -155,10 +163,12 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
                          float* dgamma, float* dbeta, int accumulate, int batch_stats,
                          float* coef, void* stream);
 
-/* dx = k1*g + k2*x + k3; dr = g (rcoef NULL, dr given) or rk1*g + rk2*r + rk3. */
+/* dx = k1*g + k2*x + k3; dr = g (rcoef NULL, dr given) or rk1*g + rk2*r + rk3;
+ * dy_coef as in sgcn_bn_bwd_reduce. */
 int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
-                      float* dx, float* dr, int B, int C, int T, int V, void* stream);
+                      const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
+                      void* stream);
 
 /* m = tanh(Feature_Mask) + 1 (shift_gcn.py:129); n = V*C. */
 int sgcn_mask_prep(const float* mask, float* m, int n, void* stream);

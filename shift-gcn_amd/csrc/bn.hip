@@ -243,20 +243,24 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
 // ------------------------------------------------------------------------------------
 // backward: reductions of g = dy*(y>0) and g*xhat per feature
 // ------------------------------------------------------------------------------------
-template <bool PER_JOINT, bool RELU, bool RESBN>
+// DYT: the incoming gradient is itself a BatchNorm input-gradient that was never
+// materialised: dy_eff = k1[c]*dy + k2[c]*y + k3[c] with y the tensor read for the ReLU
+// mask (the unit's gcn output H, input of Shift_tcn.bn).
+template <bool PER_JOINT, bool RELU, bool RESBN, bool DYT>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ r, const float* __restrict__ rmean,
-    const float* __restrict__ rinvstd, float2* __restrict__ part,
+    const float* __restrict__ rinvstd, const float* __restrict__ dyc, float2* __restrict__ part,
     float2* __restrict__ rpart, int C, int T, int V) {
   __shared__ float s0[kThreads], s1[kThreads], red[2 * kThreads / 64];
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
   const size_t off = (size_t)plane * P;
   const int i = threadIdx.x;
-  float rm = 0.f, ri = 0.f;
+  float rm = 0.f, ri = 0.f, d1 = 1.f, d2 = 0.f, d3 = 0.f;
   if (RESBN) { rm = rmean[c]; ri = rinvstd[c]; }
+  if (DYT) { d1 = dyc[c]; d2 = dyc[C + c]; d3 = dyc[2 * C + c]; }
   float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
   if (PER_JOINT) {
     const int G = kThreads / V;
@@ -276,7 +280,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-          float g = (t0 + u * G < T) ? gv[u] : 0.f;
+          float g = gv[u];
+          if (DYT) g = d1 * g + d2 * yv[u] + d3;
+          g = (t0 + u * G < T) ? g : 0.f;
           if (RELU) g = yv[u] > 0.f ? g : 0.f;
           a0 += g;
           a1 += g * ((xv[u] - mu) * is);
@@ -308,7 +314,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        float g = (base + u * kThreads + i < P) ? gv[u] : 0.f;
+        float g = gv[u];
+        if (DYT) g = d1 * g + d2 * yv[u] + d3;
+        g = (base + u * kThreads + i < P) ? g : 0.f;
         if (RELU) g = yv[u] > 0.f ? g : 0.f;
         a0 += g;
         a1 += g * ((xv[u] - mu) * is);
@@ -350,16 +358,18 @@ __global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
 }
 
 // dx = k1[f]*g + k2[f]*x + k3[f]; RES: 1 -> dr = g, 2 -> dr = rk1*g + rk2*r + rk3
-template <bool PER_JOINT, bool RELU, int RES>
+template <bool PER_JOINT, bool RELU, int RES, bool DYT>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ coef, int F, const float* __restrict__ r,
-    const float* __restrict__ rcoef, int RF, float* __restrict__ dx, float* __restrict__ dr,
-    int C, int T, int V) {
+    const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
+    float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V) {
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
   const size_t off = (size_t)plane * P;
   float k1 = 0.f, k2 = 0.f, k3 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+  float d1 = 1.f, d2 = 0.f, d3 = 0.f;
+  if (DYT) { d1 = dyc[c]; d2 = dyc[C + c]; d3 = dyc[2 * C + c]; }
   if (!PER_JOINT) { k1 = coef[c]; k2 = coef[F + c]; k3 = coef[2 * F + c]; }
   if (RES == 2) { q1 = rcoef[c]; q2 = rcoef[RF + c]; q3 = rcoef[2 * RF + c]; }
   const int dv = kThreads % V;
@@ -378,6 +388,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     for (int u = 0; u < kU; ++u) {
       const int o = base + u * kThreads + threadIdx.x;
       float g = gv[u];
+      if (DYT) g = d1 * g + d2 * yv[u] + d3;
       if (RELU) g = yv[u] > 0.f ? g : 0.f;
       if (PER_JOINT) {
         const int f = c * V + v;
@@ -579,18 +590,22 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
 
 int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x,
                        const float* mean, const float* invstd, int per_joint, const float* r,
-                       const float* rmean, const float* rinvstd, float* part, float* rpart,
-                       int B, int C, int T, int V, void* stream) {
+                       const float* rmean, const float* rinvstd, const float* dy_coef,
+                       float* part, float* rpart, int B, int C, int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   SGCN_REQUIRE(B > 0 && T > 0 && dy && x && mean && invstd && part && (y || !relu));
+  SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE((r == nullptr) == (rpart == nullptr) && (!r || (rmean && rinvstd)));
   hipStream_t st = (hipStream_t)stream;
   dim3 g(B * C);
   const bool rb = r != nullptr;
-#define SGCN_RED(PJ, RL, RB)                                                            \
-  bn_bwd_reduce_kernel<PJ, RL, RB><<<g, kThreads, 0, st>>>(dy, y, x, mean, invstd, r, rmean, \
-                                                           rinvstd, (float2*)part,        \
-                                                           (float2*)rpart, C, T, V)
+#define SGCN_RED(PJ, RL, RB)                                                                \
+  (dy_coef ? bn_bwd_reduce_kernel<PJ, RL, RB, true><<<g, kThreads, 0, st>>>(                   \
+                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
+                 (float2*)rpart, C, T, V)                                                     \
+           : bn_bwd_reduce_kernel<PJ, RL, RB, false><<<g, kThreads, 0, st>>>(                  \
+                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
+                 (float2*)rpart, C, T, V))
   if (per_joint) {
     if (relu) { if (rb) SGCN_RED(true, true, true); else SGCN_RED(true, true, false); }
     else { if (rb) SGCN_RED(true, false, true); else SGCN_RED(true, false, false); }
@@ -618,17 +633,22 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
 
 int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
-                      float* dx, float* dr, int B, int C, int T, int V, void* stream) {
+                      const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
+                      void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(dy && x && coef && dx && (y || !relu));
+  SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE(!rcoef || (r && dr));
   hipStream_t st = (hipStream_t)stream;
   const int res = dr == nullptr ? 0 : (rcoef ? 2 : 1);
   const int F = per_joint ? C * V : C;
   dim3 g(B * C);
-#define SGCN_BA(PJ, RL, RS) \
-  bn_bwd_apply_kernel<PJ, RL, RS><<<g, kThreads, 0, st>>>(dy, y, x, coef, F, r, rcoef, C, dx, dr, C, T, V)
+#define SGCN_BA(PJ, RL, RS)                                                                   \
+  (dy_coef ? bn_bwd_apply_kernel<PJ, RL, RS, true><<<g, kThreads, 0, st>>>(                      \
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V)                      \
+           : bn_bwd_apply_kernel<PJ, RL, RS, false><<<g, kThreads, 0, st>>>(                     \
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V))
 #define SGCN_BA_R(PJ, RL) \
   if (res == 0) SGCN_BA(PJ, RL, 0); else if (res == 1) SGCN_BA(PJ, RL, 1); else SGCN_BA(PJ, RL, 2)
   if (per_joint) { if (relu) { SGCN_BA_R(true, true); } else { SGCN_BA_R(true, false); } }

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(64 * WM * 2) void pw_fwd_kernel(FwdArgs p) {
   __shared__ float Bs[BK * BP];
   __shared__ short rot_out[BM];
   __shared__ float bias_s[BM];
-  __shared__ float mask_s[MASK ? kMaskFwdMax : 1];   // [v][k] feature mask table
+  extern __shared__ float mask_s[];   // [v][k] feature mask table (dynamic: V*K floats)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
   static_assert(MI >= 1 && NJ >= 1 && A_PER >= 1 && B_PER >= 1, "bad tile");
   __shared__ float As[BK * AP];
   __shared__ float Bs[BK * BP];
-  __shared__ float mask_s[MASK ? kMaskMaxV * BN : 1];   // [v][c - c0]
+  extern __shared__ float mask_s[];   // [v][c - c0] (dynamic: V*BN floats)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -455,8 +455,9 @@ template <int BM, int BK, bool AMC>
 void launch_fwd_bm(const FwdArgs& a, int B, bool mask, bool relu, bool accum, hipStream_t st) {
   constexpr int WM = BM / 32;   // one 32-row sub-tile per wave along M
   dim3 grid((a.M + BM - 1) / BM, (a.T * a.V + 127) / 128, B);
+  const size_t dyn = mask ? (size_t)a.V * a.K * sizeof(float) : 0;
 #define SGCN_PWF(MS, RL, AC) \
-  pw_fwd_kernel<BM, BK, WM, MS, RL, AC, AMC><<<grid, 64 * WM * 2, 0, st>>>(a)
+  pw_fwd_kernel<BM, BK, WM, MS, RL, AC, AMC><<<grid, 64 * WM * 2, dyn, st>>>(a)
   if (mask) {
     if (relu) { if (accum) SGCN_PWF(true, true, true); else SGCN_PWF(true, true, false); }
     else { if (accum) SGCN_PWF(true, false, true); else SGCN_PWF(true, false, false); }
@@ -560,8 +561,9 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
   a.chunks_per_split = (total + S - 1) / S;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(tiles, S);
-#define SGCN_DW(BM_, BN_)                                                           \
-  (mask ? pw_dw_kernel<BM_, BN_, BM_ / 32, 2, true><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a) \
+#define SGCN_DW(BM_, BN_)                                                                    \
+  (mask ? pw_dw_kernel<BM_, BN_, BM_ / 32, 2, true>                                           \
+              <<<grid, 64 * (BM_ / 32) * 2, (size_t)V * BN_ * sizeof(float), st>>>(a)       \
         : pw_dw_kernel<BM_, BN_, BM_ / 32, 2, false><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a))
   if (bm == 128 && bn == 128) SGCN_DW(128, 128);
   else if (bm == 128) SGCN_DW(128, 64);

@@ -179,14 +179,20 @@ __global__ __launch_bounds__(kThreads) void tshift_fwd_kernel(
 // ------------------------------------------------------------------------------------
 // backward: input gradient (reverse shift) + position-gradient plane partials
 // ------------------------------------------------------------------------------------
-template <int EPT, bool AFFINE, bool RELU_MASK, int STRIDE>
+// BNP: also emit the per-plane BatchNorm-backward partials {sum gin, sum gin*xhat},
+// xhat = (in - bn_mean[c]) * bn_invstd[c], of the BatchNorm that produced this shift's
+// input (Shift_tcn.bn before shift_in): its separate reduction pass disappears.
+template <int EPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP>
 __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
     const float* __restrict__ scale, const float* __restrict__ shift,
-    float* __restrict__ gin, float2* __restrict__ pgrad, int C, int Hb, int W, int Ho,
-    int add_half) {
+    const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
+    float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
+    int Hb, int W, int Ho, int add_half) {
   __shared__ float red[2 * kThreads / 64];
+  float bs0 = 0.f, bs1 = 0.f, bmu = 0.f, bis = 0.f;
+  if (BNP) { bmu = bn_mean[blockIdx.x % C]; bis = bn_invstd[blockIdx.x % C]; }
   const int plane = blockIdx.x;
   const int c = plane % C;
   const float* __restrict__ go = gout + (size_t)plane * Ho * W;
@@ -232,7 +238,8 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
           q[e][1] = go[ti[e].o01];
           q[e][2] = go[ti[e].o10];
           q[e][3] = go[ti[e].o11];
-          if (RELU_MASK) rin[e] = src[min(base + (s0 + e) * kThreads + (int)threadIdx.x, nb - 1)];
+          if (RELU_MASK || BNP)
+            rin[e] = src[min(base + (s0 + e) * kThreads + (int)threadIdx.x, nb - 1)];
           pos.next();
         }
 #pragma unroll
@@ -243,6 +250,11 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
           if (RELU_MASK) val = rin[e] > 0.f ? val : 0.f;
           const int o = base + (s0 + e) * kThreads + threadIdx.x;
           if (o < nb) gi[o] = val;
+          if (BNP) {
+            const float gv = o < nb ? val : 0.f;
+            bs0 += gv;
+            bs1 += gv * ((rin[e] - bmu) * bis);
+          }
         }
       }
     }
@@ -289,6 +301,10 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
   }
   block_sum2(ax, ay, red);
   if (threadIdx.x == 0) pgrad[plane] = make_float2(ax, ay);
+  if (BNP) {
+    block_sum2(bs0, bs1, red);
+    if (threadIdx.x == 0) bn_part[plane] = make_float2(bs0, bs1);
+  }
 }
 
 // mean over the batch of the per-plane sums (== mean_b then sum_w, sum_h of .cu:501-509
@@ -348,17 +364,25 @@ void launch_fwd(bool affine, bool stats, const float* in, float* out, const floa
 
 template <int EPT, int STRIDE>
 void launch_bwd(bool affine, bool relu, const float* gout, const float* in, const float* xpos,
-                const float* ypos, const float* scale, const float* shift, float* gin,
-                float2* pg, int B, int C, int H, int W, int Ho, int add_half, hipStream_t st) {
+                const float* ypos, const float* scale, const float* shift, const float* bmu,
+                const float* bis, float* gin, float2* pg, float2* bp, int B, int C, int H,
+                int W, int Ho, int add_half, hipStream_t st) {
   dim3 grid(B * C), block(kThreads);
-#define SGCN_BWD(A, R)                                                                      \
-  tshift_bwd_kernel<EPT, A, R, STRIDE><<<grid, block, 0, st>>>(gout, in, xpos, ypos, scale, \
-                                                               shift, gin, pg, C, H, W, Ho, \
-                                                               add_half)
-  if (affine) {
-    if (relu) SGCN_BWD(true, true); else SGCN_BWD(true, false);
+#define SGCN_BWD(A, R, P)                                                                    \
+  tshift_bwd_kernel<EPT, A, R, STRIDE, P><<<grid, block, 0, st>>>(                            \
+      gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, Ho, add_half)
+  if (bp) {
+    if (affine) {
+      if (relu) SGCN_BWD(true, true, true); else SGCN_BWD(true, false, true);
+    } else {
+      if (relu) SGCN_BWD(false, true, true); else SGCN_BWD(false, false, true);
+    }
   } else {
-    if (relu) SGCN_BWD(false, true); else SGCN_BWD(false, false);
+    if (affine) {
+      if (relu) SGCN_BWD(true, true, false); else SGCN_BWD(true, false, false);
+    } else {
+      if (relu) SGCN_BWD(false, true, false); else SGCN_BWD(false, false, false);
+    }
   }
 #undef SGCN_BWD
 }
@@ -400,7 +424,8 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C) { return (size_t)B * C * sizeof(float2); }
 
 int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const float* ypos,
-                    const float* in_scale, const float* in_shift, int relu_mask, float* gin,
+                    const float* in_scale, const float* in_shift, int relu_mask,
+                    const float* bn_mean, const float* bn_invstd, float* bn_part, float* gin,
                     float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                     int W, int stride, int ypos_is_raw, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H >= 0 && W > 0 && (stride == 1 || stride == 2));
@@ -408,18 +433,20 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   const int Ho = H / stride;
   SGCN_REQUIRE((gout || Ho == 0) && (in || H == 0) && (gin || H == 0));
   SGCN_REQUIRE(xpos && ypos && gx && gy && ws);
+  SGCN_REQUIRE(!bn_part || (bn_mean && bn_invstd));
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
   SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const bool aff = in_scale != nullptr, relu = relu_mask != 0;
   float2* pg = (float2*)ws;
+  float2* bp = (float2*)bn_part;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
   const int ept = pick_ept(H * W);
 #define SGCN_BWD_EPT(E)                                                                     \
-  (stride == 1 ? launch_bwd<E, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, gin, \
-                                  pg, B, C, H, W, Ho, ah, st)                                   \
-               : launch_bwd<E, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, gin, \
-                                  pg, B, C, H, W, Ho, ah, st))
+  (stride == 1 ? launch_bwd<E, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, \
+                                  bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st)                                   \
+               : launch_bwd<E, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, \
+                                  bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st))
   if (ept == 8) SGCN_BWD_EPT(8); else if (ept == 16) SGCN_BWD_EPT(16); else SGCN_BWD_EPT(32);
 #undef SGCN_BWD_EPT
   SGCN_LAUNCH_CHECK();

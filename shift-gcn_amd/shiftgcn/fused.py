@@ -16,8 +16,10 @@ Shift_tcn (shift_gcn.py:65-74)
   fwd : moments -> finalize(bn) -> tshift_fwd[bn affine fused on taps]
         -> pw_fwd[temporal_linear + bias + ReLU] -> tshift_fwd[stride s, bn2 moments fused]
         -> finalize(bn2) -> (standalone: bn_apply)
-  bwd : tshift_bwd[ReLU mask fused] -> pw_dw -> pw_fwd(dX) -> tshift_bwd[bn affine]
-        -> bn_bwd_reduce -> finalize -> bn_bwd_apply
+  bwd : tshift_bwd[ReLU mask fused] -> pw_dw -> pw_fwd(dX)
+        -> tshift_bwd[bn affine + bn-backward partials fused] -> finalize
+        -> (standalone: bn_bwd_apply; in a unit the BN input gradient is never written: the
+           gcn BN-backward kernels evaluate it on the fly)
 TCN_GCN_unit (shift_gcn.py:160-162): bn2 apply + residual (0 / identity / tcn conv+BN) +
   ReLU is ONE bn_apply launch; its backward ONE reduce + ONE apply.
 
@@ -72,17 +74,20 @@ def gcn_forward(mod, x0, training):
     return H, s
 
 
-def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None):
-    """Returns (dx0, {param_name: grad})."""
+def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None):
+    """Returns (dx0, {param_name: grad}). With ``dy_coef`` ([3, Cout]) the incoming
+    gradient is dH = k1*dH_arg + k2*H + k3 (Shift_tcn.bn's input gradient), evaluated
+    on the fly by the BN-backward kernels instead of being materialised."""
     x0 = s.x0
     B, Cin, T, V = x0.shape
     Cout = mod.out_channels
     g = {}
     if mod.has_down:
         conv, bnd = mod.down[0], mod.down[1]
-        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, r=s.D0, rst=s.dst)
+        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, r=s.D0, rst=s.dst,
+                                        dy_coef=dy_coef)
     else:
-        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True)
+        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, dy_coef=dy_coef)
     coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, Cout * V, B * T, s.zst,
                                                                mod.bn, perm_V=V)
     dZ = _empty(B, Cout, T, V, like=x0)
@@ -91,10 +96,11 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None):
         coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
             rpart, B, Cout, B * T * V, s.dst, bnd)
         dD0 = _empty(B, Cout, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ,
+                         dy_coef=dy_coef)
     else:
         g_id = _empty(B, Cin, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, dr=g_id, dx=dZ)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, dr=g_id, dx=dZ, dy_coef=dy_coef)
     # einsum/bias grads: G(b,d,n) = dZ gathered back through shift_out (rotation +d)
     dLW = torch.empty_like(mod.Linear_weight)
     dLb = torch.empty_like(mod.Linear_bias)
@@ -152,8 +158,9 @@ def tcn_core_forward(mod, H, training, h_moments=None):
     return S, sst, s
 
 
-def tcn_core_backward(mod, s: TcnSaved, dS):
-    """dS: gradient w.r.t. S (pre-bn2). Returns (dH, grads)."""
+def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True):
+    """dS: gradient w.r.t. S (pre-bn2). Returns (dH, grads), or ((dA, coef), grads) with
+    ``materialize_dx=False`` (dH = coef[0]*dA + coef[1]*H + coef[2], fused downstream)."""
     H = s.H
     B, C, T, V = H.shape
     Cout = mod.out_channels
@@ -168,12 +175,14 @@ def tcn_core_backward(mod, s: TcnSaved, dS):
     g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
     dAs = _empty(B, C, T, V, like=H)
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
-    dA, g["shift_in.xpos"], g["shift_in.ypos"] = ops.tshift_bwd(
+    # shift_in backward with Shift_tcn.bn's backward partials fused in
+    dA, g["shift_in.xpos"], g["shift_in.ypos"], part = ops.tshift_bwd(
         dAs, H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=s.ast.scale,
-        shift=s.ast.shift)
-    part, _ = ops.bn_bwd_reduce(dA, None, False, H, s.ast, False)
+        shift=s.ast.shift, bn_stats=s.ast)
     coef, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, C, B * T * V, s.ast,
                                                              mod.bn)
+    if not materialize_dx:
+        return (dA, coef), g       # dH = k1*dA + k2*H + k3, left for the consumer to fuse
     dH = ops.bn_bwd_apply(dA, None, False, H, coef, False)
     return dH, g
 
@@ -264,9 +273,10 @@ def unit_backward(unit, s: UnitSaved, dout):
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dr=dres, dx=dS)
     else:
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dx=dS)
-    dH, gt = tcn_core_backward(unit.tcn1, ts, dS)
+    (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, dS, materialize_dx=False)
     g.update({"tcn1." + k: v for k, v in gt.items()})
-    dx, gg = gcn_backward(unit.gcn1, s.gs, dH, extra_dx=dres if kind == "identity" else None)
+    dx, gg = gcn_backward(unit.gcn1, s.gs, dA, extra_dx=dres if kind == "identity" else None,
+                          dy_coef=coefA)
     g.update({"gcn1." + k: v for k, v in gg.items()})
     if kind == "conv":
         gr = convbn_dx_and_dw(unit.residual, s.rs, dres, dx, accumulate=True)

@@ -125,8 +125,9 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
 
 
 def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=False,
-               ypos_is_raw=True):
-    """Backward shift: returns (grad_input, grad_xpos, grad_ypos)."""
+               ypos_is_raw=True, bn_stats=None):
+    """Backward shift: returns (grad_input, grad_xpos, grad_ypos), plus the BatchNorm
+    backward partials of ``bn_stats`` (the BN whose output feeds the shift) if given."""
     check_input(gout, "grad_output")
     check_input(inp, "input")
     check_input(xpos, "xpos")
@@ -140,13 +141,18 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     gy = torch.empty((C,), device=dev, dtype=_F32)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
+    bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if bn_stats is not None else None
     nb = 4 * (gout.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp):
         rc = lib.sgcn_tshift_bwd(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos), _ptr(scale),
-                                 _ptr(shift), int(bool(relu_mask)), _ptr(gin), _ptr(gx),
-                                 _ptr(gy), _ptr(ws), nbytes, B, C, H, W, stride,
-                                 int(ypos_is_raw), _stream(inp))
+                                 _ptr(shift), int(bool(relu_mask)),
+                                 _ptr(bn_stats.mean) if bn_stats is not None else None,
+                                 _ptr(bn_stats.invstd) if bn_stats is not None else None,
+                                 _ptr(bpart), _ptr(gin), _ptr(gx), _ptr(gy), _ptr(ws), nbytes,
+                                 B, C, H, W, stride, int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd")
+    if bn_stats is not None:
+        return gin, gx, gy, bpart
     return gin, gx, gy
 
 
@@ -272,7 +278,8 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
     return y if out_stats is None else (y, ys)
 
 
-def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats = None):
+def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats = None,
+                  dy_coef=None):
     check_input(dy, "grad_output")
     B, C, T, V = x.shape
     dev = x.device
@@ -281,8 +288,8 @@ def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats =
     rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(st.mean),
                                         _ptr(st.invstd), int(per_joint), _ptr(r),
                                         _ptr(rst.mean) if rst else None,
-                                        _ptr(rst.invstd) if rst else None, _ptr(part),
-                                        _ptr(rpart), B, C, T, V, _stream(x))
+                                        _ptr(rst.invstd) if rst else None, _ptr(dy_coef),
+                                        _ptr(part), _ptr(rpart), B, C, T, V, _stream(x))
     _lib.check(rc, "sgcn_bn_bwd_reduce")
     return part, rpart
 
@@ -301,12 +308,13 @@ def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
     return coef, dgamma, dbeta
 
 
-def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, dx=None):
+def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, dx=None,
+                 dy_coef=None):
     B, C, T, V = x.shape
     dx = torch.empty_like(x) if dx is None else dx
     rc = _lib.load().sgcn_bn_bwd_apply(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(coef),
-                                       int(per_joint), _ptr(r), _ptr(rcoef), _ptr(dx),
-                                       _ptr(dr), B, C, T, V, _stream(x))
+                                       int(per_joint), _ptr(r), _ptr(rcoef), _ptr(dy_coef),
+                                       _ptr(dx), _ptr(dr), B, C, T, V, _stream(x))
     _lib.check(rc, "sgcn_bn_bwd_apply")
     return dx
 

@@ -41,7 +41,7 @@ def test_invalid_arguments_rejected_before_launch():
     assert lib.sgcn_tshift_fwd(None, None, None, None, None, None, None, 2, 3, 4, 5, 0, 1,
                                None) == _lib.EINVAL
     assert lib.sgcn_tshift_bwd(None, None, None, None, None, None, 0, None, None, None, None,
-                               0, 2, 3, 4, 5, 3, 1, None) == _lib.EINVAL
+                               None, None, None, 0, 2, 3, 4, 5, 3, 1, None) == _lib.EINVAL
     assert lib.sgcn_tshift_bwd_ws_bytes(4, 8) == 4 * 8 * 8
 
 
