@@ -13,16 +13,19 @@
 // channel). No permute to (n·t, v·c) is ever materialised.
 //
 // Kernels
-//  * pw_fwd_kernel : Y[b][m][pos_out(n,m)] (+)= act(sum_k A[m][k] * Bop(b,k,n) + bias[m])
-//      used for the forward (A = weights) and for dX (A = weights^T).
-//      Tile BM x 128 positions x BK, 4 waves (2x2), v_mfma_f32_32x32x2_f32 (exact f32,
-//      one rounding per product == an fmaf chain), LDS-staged operands with register
-//      prefetch of the next K stage, M-tiles fastest in the grid so the blocks sharing an
-//      X tile run back to back (Infinity-Cache hits for the second M-tile).
+//  * pwg_fwd_kernel : Y[b][m][pos_out(n,m)] (+)= act(sum_k A[m][k] * Bop(b,k,n) + bias[m])
+//      used for the forward (A = weights) and for dX (A = weights^T). Positions are
+//      flattened over (sample, t, v); one tile = all M (<= 256) x BN positions, so the X
+//      operand crosses HBM exactly once in long contiguous runs per channel row.
+//      v_mfma_f32_32x32x2_f32 (exact f32, one rounding per product == an fmaf chain),
+//      BK = 16 double-buffered LDS stages (one barrier per stage), register prefetch of
+//      the next stage's global loads while the current stage's MFMAs issue.
 //  * pw_dw_kernel  : split-K dW[m][n] = sum_{b,p} G(b,m,p) * X(b,n,p) over all positions,
 //      deterministic fp32 partial slabs [split][M][N] + row sums (bias grad), reduced in
 //      fixed order by slab_reduce_kernel (optionally transposed, for Linear_weight's
 //      (C_in, C_out) layout).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace sgcn {
@@ -30,9 +33,7 @@ namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int kThreads = 256;
-constexpr int kMaskMaxV = 64;      // joints per row supported by the dW LDS mask table
-constexpr int kMaskFwdMax = 8448;  // V*K floats of the forward LDS mask table (33 x 256)
+constexpr int kMaskMaxV = 64;      // joints per row supported by the LDS mask tables
 
 // A position-mapped plane operand: element (b, ch, n) with n = t*V + v (logical
 // position) lives at ptr[b*bstride + ch*cstride + (t*tstride)*V + rot(v, ch)], where
@@ -62,6 +63,11 @@ struct FwdArgs {
   const float* mask;  // optional mask[v*K + k] multiplied into B (Shift_gcn feature mask)
   OutPlane y;
   int M, K, T, V;
+  int B;
+  // byte extents of the operands (buffer-descriptor ranges: an offset at or past the
+  // extent loads 0 / drops the store) and epilogue flags
+  unsigned x_bytes, y_bytes, a_bytes, mask_bytes;
+  int relu;
 };
 
 __device__ __forceinline__ int pmod(int a, int V) {
@@ -75,98 +81,139 @@ __device__ __forceinline__ float keep(float v, bool ok) {
   return __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
 }
 
+// buffer descriptor over [base, base + bytes): 32-bit per-lane voffset + wave-uniform
+// soffset, hardware range check (out-of-range loads return 0, stores are dropped)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, unsigned voff,
+                                       unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+}
+
 // rotation step (d*rsign) mod V in [0, V)
 __device__ __forceinline__ int rot_step(int d, int rsign, int V) { return pmod(d * rsign, V); }
 
 // ------------------------------------------------------------------------------------
-// forward / dX
+// forward / dX. Positions are flattened over (sample, t, v) so a tile may span samples;
+// one tile = all M (<= BM) x BN positions, so X crosses HBM once in long contiguous
+// runs per channel row; BK = 16 double-buffered LDS stages, one barrier per stage.
+// The main loop is VALU-lean: on gfx950 the f32 MFMA
+// runs on the vector ALU: every VALU instruction between MFMAs costs MFMA issue time
+// (measured: 2 v_fma per v_mfma_f32_32x32x2_f32 -> -15 %, 8 -> -35 %). So operands
+// are fetched with buffer loads whose per-lane byte offset is fixed for the whole tile
+// (the (sample, t[, v]) column) and whose row offset (channel, K-stage) is a wave-
+// uniform SGPR soffset; bounds come from the descriptor range (out-of-range -> 0), not
+// from per-element selects. Only the joint-shift rotation (XROT) and the feature mask
+// cost VALU per loaded element.
 // ------------------------------------------------------------------------------------
-template <int BM, int BK, int WM, bool MASK, bool RELU, bool ACCUM, bool AMC>
-__global__ __launch_bounds__(64 * WM * 2) void pw_fwd_kernel(FwdArgs p) {
-  constexpr int NT = 64 * WM * 2;      // waves: WM along M x 2 along N
-  constexpr int BN = 128;
-  constexpr int MI = BM / WM / 32;     // 32-row sub-tiles per wave
-  constexpr int NJ = BN / 2 / 32;      // 32-col sub-tiles per wave
+template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM>
+__global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BK = 16;
+  constexpr int MI = BM / WM / 32;
+  constexpr int NJ = BN / WN / 32;
   constexpr int AP = BM + 1, BP = BN + 1;
   constexpr int A_PER = BM * BK / NT;
   constexpr int B_PER = BN * BK / NT;
-  constexpr int KSTEP_B = NT / BN;     // k rows between a thread's B elements
-  static_assert(MI >= 1, "wave tile too small");
-  static_assert(A_PER >= 1 && B_PER >= 1, "tile too small");
-  __shared__ float As[BK * AP];
-  __shared__ float Bs[BK * BP];
-  __shared__ short rot_out[BM];
+  constexpr int KSTEP_B = NT / BN;
+  static_assert(MI >= 1 && NJ >= 1 && A_PER >= 1 && B_PER >= 1, "bad tile");
+  static_assert((BM * BK) % NT == 0 && NT % BN == 0 && NT % BK == 0 && NT % BM == 0, "bad tile");
+  __shared__ float As[2][BK * AP];
+  __shared__ float Bs[2][BK * BP];
   __shared__ float bias_s[BM];
-  extern __shared__ float mask_s[];   // [v][k] feature mask table (dynamic: V*K floats)
+  __shared__ int rot_s[BM];
+  __shared__ unsigned ycol_s[BN];   // per tile column: byte offset of (b, t) in Y
+  __shared__ int v_s[BN];           // per tile column: joint v
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int V = p.V, N = p.T * V, K = p.K, M = p.M;
+  const int P = p.B * N;                 // < 2^31 (host-checked)
+  const int p0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * BM;
+  const auto xr = make_rsrc(p.x.ptr, p.x_bytes);
+  const auto ar = make_rsrc(p.A, p.a_bytes);
+  const auto mr = make_rsrc(MASK ? p.mask : p.A, MASK ? p.mask_bytes : 0u);
 
-  // row-constant epilogue data staged once (no runtime-conditional load in the epilogue)
   for (int i = tid; i < BM; i += NT) {
-    rot_out[i] = (short)pmod(p.y.rsign * (m0 + i), V);
     bias_s[i] = (p.bias && m0 + i < M) ? p.bias[m0 + i] : 0.f;
+    rot_s[i] = pmod(p.y.rsign * (m0 + i), V);
   }
-  if (MASK)
-    for (int i = tid; i < V * K; i += NT) mask_s[i] = p.mask[i];
-  __syncthreads();   // rot_out / bias_s / mask_s are read before the main loop's barrier
 
-  // B staging: thread owns column n and rows kb0 + KSTEP_B*i. 32-bit offsets from the
-  // sample's base; the shift_in rotation (v + rsign*k) mod V advances incrementally.
-  const int nb = tid % BN, kb0 = tid / BN;
-  const int n = n0 + nb;
-  const bool nvalid = n < N;
-  const int ncl = min(n, N - 1);
-  const int tt = ncl / V;
-  const int vv = ncl - tt * V;
-  const float* __restrict__ xb =
-      p.x.ptr + (long long)b * p.x.bstride + (long long)tt * p.x.tstride * V;
-  const int xcs = (int)p.x.cstride;
-  const int bstep = rot_step(KSTEP_B, p.x.rsign, V);
-  // A staging
-  constexpr int A_MSTEP = NT / BK;   // (k-contig) rows per step
-  constexpr int A_KSTEP = NT / BM;   // (m-contig) k per step
+  // ---- B column of this thread (fixed for the tile) ----
+  const int nb = tid % BN;
+  const int kb0 = __builtin_amdgcn_readfirstlane(tid / BN);
+  int vv = 0;
+  unsigned xcol = p.x_bytes;   // out of range: loads return 0
+  {
+    const int pc = p0 + nb;
+    unsigned ycol = p.y_bytes;   // out of range: stores dropped
+    if (pc < P) {
+      const int b = pc / N;
+      const int n = pc - b * N;
+      const int t = n / V;
+      vv = n - t * V;
+      xcol = (unsigned)(((long long)b * p.x.bstride + (long long)t * p.x.tstride * V +
+                         (XROT ? 0 : vv)) * 4);
+      ycol = (unsigned)(((long long)b * p.y.bstride + (long long)t * p.y.tstride * V) * 4);
+    }
+    if (tid < BN) {
+      ycol_s[nb] = ycol;
+      v_s[nb] = vv;
+    }
+  }
+  const unsigned xcs4 = (unsigned)(p.x.cstride * 4);
+  const int bstep = XROT ? rot_step(KSTEP_B, p.x.rsign, V) : 0;
+  const int kstage_rot = XROT ? rot_step(BK, p.x.rsign, V) : 0;
+  int cv0 = XROT ? pmod(vv + p.x.rsign * kb0, V) : 0;
+  const unsigned mcol = (unsigned)(vv * K * 4);
+
+  // ---- A element of this thread: (m, k) = fixed lane part + uniform i part ----
+  const int lda = p.lda;
   const int am = AMC ? tid % BM : tid / BK;
   const int ak = AMC ? tid / BM : tid % BK;
-  const float* __restrict__ A = p.A;
-  const int lda = p.lda;
+  const unsigned avoff = AMC ? (m0 + am < M ? (unsigned)((ak * lda + m0 + am) * 4) : p.a_bytes)
+                             : (unsigned)(((m0 + am) * lda + ak) * 4);
+  // per-i uniform step of the A element: AMC -> k += NT/BM, else m += NT/BK
+  const unsigned astep = AMC ? (unsigned)((NT / BM) * lda * 4) : (unsigned)((NT / BK) * lda * 4);
 
-  // Raw loads only (always in bounds); validity is applied at the LDS store, after the
-  // MFMAs of the current stage, so no instruction consumes a prefetched value early
-  // (consuming it right away made hipcc drain vmcnt(0) after every load).
-  float ra[A_PER], rb[B_PER];
+  float ra[A_PER], rb[B_PER], rm[MASK ? B_PER : 1];
   auto load_stage = [&](int k0) {
-    int cv = pmod(vv + p.x.rsign * (k0 + kb0), V);
+    int cv = cv0;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int kc = min(k0 + kb0 + i * KSTEP_B, K - 1);
-      rb[i] = xb[kc * xcs + cv];
-      cv += bstep;
-      cv = cv >= V ? cv - V : cv;
+      const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
+      const unsigned voff = XROT ? xcol + (unsigned)(cv * 4) : xcol;
+      rb[i] = bload(xr, voff, (unsigned)row * xcs4);
+      if (MASK) rm[i] = bload(mr, mcol, (unsigned)row * 4u);
+      if (XROT) {
+        cv += bstep;
+        cv = cv >= V ? cv - V : cv;
+      }
     }
+    const unsigned ak0 = AMC ? (unsigned)(k0 * lda * 4) : (unsigned)(k0 * 4);
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int m = AMC ? am : am + i * A_MSTEP;
-      const int k = AMC ? ak + i * A_KSTEP : ak;
-      const int gmc = min(m0 + m, M - 1), gkc = min(k0 + k, K - 1);
-      ra[i] = AMC ? A[gkc * lda + gmc] : A[gmc * lda + gkc];
-    }
+    for (int i = 0; i < A_PER; ++i) ra[i] = bload(ar, avoff, ak0 + (unsigned)i * astep);
   };
-  auto store_stage = [&](int kst) {
+  auto store_stage = [&](int buf, int k0) {
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int k = kst + kb0 + i * KSTEP_B;
-      float v = keep(rb[i], nvalid && k < K);
-      if (MASK) v *= mask_s[vv * K + min(k, K - 1)];
-      Bs[(kb0 + i * KSTEP_B) * BP + nb] = v;
+    for (int i = 0; i < B_PER; ++i)
+      Bs[buf][(kb0 + i * KSTEP_B) * BP + nb] = MASK ? rb[i] * rm[i] : rb[i];
+    if (!AMC && k0 + BK > K) {   // k-contiguous A: a k past K aliases the next row
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) ra[i] = keep(ra[i], k0 + ak < K);
     }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int m = AMC ? am : am + i * A_MSTEP;
-      const int k = AMC ? ak + i * A_KSTEP : ak;
-      As[k * AP + m] = keep(ra[i], m0 + m < M && kst + k < K);
+      const int m = AMC ? am : am + i * (NT / BK);
+      const int k = AMC ? ak + i * (NT / BM) : ak;
+      As[buf][k * AP + m] = ra[i];
     }
   };
 
@@ -177,78 +224,96 @@ __global__ __launch_bounds__(64 * WM * 2) void pw_fwd_kernel(FwdArgs p) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
 
   const int kl = lane >> 5, cl = lane & 31;
+  const int nstage = (K + BK - 1) / BK;
   load_stage(0);
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    store_stage(k0);
-    __syncthreads();
-    if (k0 + BK < K) load_stage(k0 + BK);
-    // fragments double-buffered in registers: the LDS reads of k-step kk+2 are in
-    // flight while the MFMAs of k-step kk issue (no lgkmcnt(0) stall per k-step)
+  store_stage(0, 0);
+  __syncthreads();
+  for (int s = 0; s < nstage; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nstage) {
+      if (XROT) {
+        cv0 += kstage_rot;
+        cv0 = cv0 >= V ? cv0 - V : cv0;
+      }
+      load_stage((s + 1) * BK);
+    }
+    const float* __restrict__ Aw = As[cur] + kl * AP + wm * (BM / WM) + cl;
+    const float* __restrict__ Bw = Bs[cur] + kl * BP + wn * (BN / WN) + cl;
     float af[2][MI], bf[2][NJ];
-    const float* __restrict__ Aw = As + kl * AP + wm * (BM / WM) + cl;
-    const float* __restrict__ Bw = Bs + kl * BP + wn * (BN / 2) + cl;
 #pragma unroll
     for (int i = 0; i < MI; ++i) af[0][i] = Aw[i * 32];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) bf[0][j] = Bw[j * 32];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      const int cur = (kk >> 1) & 1;
+      const int c2 = (kk >> 1) & 1;
       if (kk + 2 < BK) {
 #pragma unroll
-        for (int i = 0; i < MI; ++i) af[cur ^ 1][i] = Aw[(kk + 2) * AP + i * 32];
+        for (int i = 0; i < MI; ++i) af[c2 ^ 1][i] = Aw[(kk + 2) * AP + i * 32];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bf[cur ^ 1][j] = Bw[(kk + 2) * BP + j * 32];
+        for (int j = 0; j < NJ; ++j) bf[c2 ^ 1][j] = Bw[(kk + 2) * BP + j * 32];
       }
-      // keep the prefetch reads above this k-step's MFMAs (the scheduler otherwise sinks
-      // them below to reuse registers, exposing LDS latency every k-step)
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][i], bf[cur][j], acc[i][j],
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[c2][i], bf[c2][j], acc[i][j],
                                                            0, 0, 0);
     }
+    if (s + 1 < nstage) store_stage(cur ^ 1, (s + 1) * BK);
     __syncthreads();
   }
 
-  // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-  // Row-constant data (bias, output rotation) per register; stores are predicated, never
-  // branched around a load (ACCUM loads everything first).
-  float* __restrict__ yb = p.y.ptr + (long long)b * p.y.bstride;
-  const int ycs = (int)p.y.cstride;
+  // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5) ----
+  const auto yr = make_rsrc(p.y.ptr, p.y_bytes);
+  const unsigned ycs4 = (unsigned)(p.y.cstride * 4);
+  const bool slow = p.y.rsign != 0 || m0 + BM > M;
+  const int rbase = wm * (BM / WM) + 4 * kl;   // row of register 0 of sub-tile 0 (tile-local)
+  auto epilogue = [&](auto relu_tag) {
+    constexpr bool RELU = decltype(relu_tag)::value;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = n0 + wn * (BN / 2) + j * 32 + cl;
-    const bool cok = col < N;
-    const int colc = min(col, N - 1);
-    const int t = colc / V, v = colc - t * V;
-    const int rowoff = t * p.y.tstride * V;
+    for (int j = 0; j < NJ; ++j) {
+      const int cidx = wn * (BN / WN) + j * 32 + cl;
+      const unsigned ycol = ycol_s[cidx];
+      const int v = v_s[cidx];
+      const unsigned lanerow = (unsigned)(4 * kl) * ycs4;
+      if (!slow) {
+        const unsigned voff = ycol + (unsigned)(v * 4) + lanerow;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      int off[16];
-      float prev[16];
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        const int mc = min(m0 + row, M - 1);
-        int vo = v + rot_out[row];
-        vo = vo >= V ? vo - V : vo;
-        off[r] = mc * ycs + rowoff + vo;
-        if (ACCUM) prev[r] = yb[off[r]];
-      }
+          for (int r = 0; r < 16; ++r) {
+            const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2);   // uniform
+            const unsigned soff = (unsigned)(m0 + rl) * ycs4;
+            float val = acc[i][j][r] + bias_s[rbase + i * 32 + (r & 3) + 8 * (r >> 2)];
+            if (RELU) val = fmaxf(val, 0.f);
+            if (ACCUM) val += bload(yr, voff, soff);
+            bstore(yr, val, voff, soff);
+          }
+      } else {
+        // shift_out rotation of the stored joint and/or rows past M
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        const int m = m0 + row;
-        float val = acc[i][j][r] + bias_s[row];
-        if (RELU) val = fmaxf(val, 0.f);
-        if (ACCUM) val += prev[r];
-        if (cok && m < M) yb[off[r]] = val;
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2);   // uniform
+            const int row = rl + 4 * kl;
+            int vo = v + rot_s[row];
+            vo = vo >= V ? vo - V : vo;
+            const unsigned voff =
+                (m0 + row < M ? ycol + (unsigned)(vo * 4) : p.y_bytes) + lanerow;
+            const unsigned soff = (unsigned)(m0 + rl) * ycs4;
+            float val = acc[i][j][r] + bias_s[row];
+            if (RELU) val = fmaxf(val, 0.f);
+            if (ACCUM) val += bload(yr, voff, soff);
+            bstore(yr, val, voff, soff);
+          }
       }
     }
-  }
+  };
+  if (p.relu) epilogue(std::true_type{});
+  else epilogue(std::false_type{});
 }
 
 // ------------------------------------------------------------------------------------
@@ -451,21 +516,29 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // ------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------
-template <int BM, int BK, bool AMC>
-void launch_fwd_bm(const FwdArgs& a, int B, bool mask, bool relu, bool accum, hipStream_t st) {
-  constexpr int WM = BM / 32;   // one 32-row sub-tile per wave along M
-  dim3 grid((a.M + BM - 1) / BM, (a.T * a.V + 127) / 128, B);
-  const size_t dyn = mask ? (size_t)a.V * a.K * sizeof(float) : 0;
-#define SGCN_PWF(MS, RL, AC) \
-  pw_fwd_kernel<BM, BK, WM, MS, RL, AC, AMC><<<grid, 64 * WM * 2, dyn, st>>>(a)
-  if (mask) {
-    if (relu) { if (accum) SGCN_PWF(true, true, true); else SGCN_PWF(true, true, false); }
-    else { if (accum) SGCN_PWF(true, false, true); else SGCN_PWF(true, false, false); }
-  } else {
-    if (relu) { if (accum) SGCN_PWF(false, true, true); else SGCN_PWF(false, true, false); }
-    else { if (accum) SGCN_PWF(false, false, true); else SGCN_PWF(false, false, false); }
-  }
-#undef SGCN_PWF
+template <int BM, int BN, int WM, int WN>
+void launch_pwg(const FwdArgs& a, bool accum, hipStream_t st) {
+  const long long P = (long long)a.B * a.T * a.V;   // < 2^31 (checked by the caller)
+  dim3 grid((unsigned)((P + BN - 1) / BN), (a.M + BM - 1) / BM);
+  const bool mask = a.mask != nullptr, xrot = a.x.rsign != 0, amc = a.a_mcontig != 0;
+#define SGCN_PWG(MS, XR, AM, AC) \
+  pwg_fwd_kernel<BM, BN, WM, WN, MS, XR, AM, AC><<<grid, 64 * WM * WN, 0, st>>>(a)
+#define SGCN_PWG_AC(MS, XR, AM) \
+  (accum ? SGCN_PWG(MS, XR, AM, true) : SGCN_PWG(MS, XR, AM, false))
+#define SGCN_PWG_AM(MS, XR) (amc ? SGCN_PWG_AC(MS, XR, true) : SGCN_PWG_AC(MS, XR, false))
+  if (mask) { if (xrot) SGCN_PWG_AM(true, true); else SGCN_PWG_AM(true, false); }
+  else { if (xrot) SGCN_PWG_AM(false, true); else SGCN_PWG_AM(false, false); }
+#undef SGCN_PWG_AM
+#undef SGCN_PWG_AC
+#undef SGCN_PWG
+}
+
+// byte extent of a plane operand: one past its last addressed element
+unsigned plane_bytes(long long bstride, long long cstride, int tstride, int B, int C, int T,
+                     int V) {
+  const long long e = (long long)(B - 1) * bstride + (long long)(C - 1) * cstride +
+                      (long long)(T - 1) * tstride * V + V;
+  return (unsigned)(e * 4);
 }
 
 int dw_splits(int M, int Nc, int B, int N, int tiles) {
@@ -496,7 +569,11 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   SGCN_REQUIRE(x_tstride >= 1 && y_tstride >= 1);
   SGCN_REQUIRE(x_rsign >= -1 && x_rsign <= 1 && y_rsign >= -1 && y_rsign <= 1);
   SGCN_REQUIRE(x_cstride * (long long)K < (1LL << 31) && y_cstride * (long long)M < (1LL << 31));
-  SGCN_REQUIRE(!mask || V * K <= kMaskFwdMax);
+  SGCN_REQUIRE(!mask || V <= kMaskMaxV);
+  SGCN_REQUIRE((long long)B * T * V < (1LL << 31));
+  // operand extents must fit the 32-bit buffer ranges
+  SGCN_REQUIRE((long long)(B - 1) * x_bstride + (long long)K * x_cstride + (long long)T * x_tstride * V < (1LL << 29));
+  SGCN_REQUIRE((long long)(B - 1) * y_bstride + (long long)M * y_cstride + (long long)T * y_tstride * V < (1LL << 29));
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(w && x && y);
   FwdArgs a;
@@ -511,17 +588,17 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   a.K = K;
   a.T = T;
   a.V = V;
+  a.B = B;
   hipStream_t st = (hipStream_t)stream;
   const bool mk = mask != nullptr, rl = relu != 0, ac = accumulate != 0;
-#define SGCN_FWD_BM(BM_, BK_)                                                       \
-  (w_mcontig ? launch_fwd_bm<BM_, BK_, true>(a, B, mk, rl, ac, st)                  \
-             : launch_fwd_bm<BM_, BK_, false>(a, B, mk, rl, ac, st))
-  if (K <= 4) {
-    if (M <= 64) SGCN_FWD_BM(64, 4); else SGCN_FWD_BM(128, 4);
-  } else {
-    if (M <= 64) SGCN_FWD_BM(64, 32); else SGCN_FWD_BM(128, 32);
-  }
-#undef SGCN_FWD_BM
+  a.x_bytes = plane_bytes(x_bstride, x_cstride, x_tstride, B, K, T, V);
+  a.y_bytes = plane_bytes(y_bstride, y_cstride, y_tstride, B, M, T, V);
+  a.a_bytes = (unsigned)((long long)M * K * 4);
+  a.mask_bytes = mask ? (unsigned)(V * K * 4) : 0u;
+  a.relu = rl ? 1 : 0;
+  if (M <= 64) launch_pwg<64, 256, 2, 4>(a, ac, st);
+  else if (M <= 128) launch_pwg<128, 256, 2, 4>(a, ac, st);
+  else launch_pwg<256, 128, 4, 2>(a, ac, st);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

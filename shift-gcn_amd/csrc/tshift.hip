@@ -307,6 +307,198 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// LDS-staged variants (the product path whenever the plane fits): every element of the
+// plane(s) crosses HBM exactly once with fully coalesced dword loads, and the four taps
+// of each output are LDS reads (conflict-free: a wave reads 64 consecutive words).
+// Same expressions in the same order as the global-tap kernels above, so the results
+// are bit-identical to them (and to the oracle).
+// ------------------------------------------------------------------------------------
+constexpr int kFwdLdsMax = 8192;    // floats of the staged input plane (32 KiB)
+constexpr int kBwdLdsMax = 16384;   // floats of the staged gout + input planes (64 KiB)
+
+// copy n floats src -> lds (optionally x*a+b), all loads of a thread issued before any
+// LDS store; n <= LPT * NT
+template <int NT, int LPT, bool AFFINE>
+__device__ __forceinline__ void stage_plane(const float* __restrict__ src, float* lds, int n,
+                                            float a, float b) {
+  float t[LPT];
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) t[e] = src[min(e * NT + (int)threadIdx.x, n - 1)];
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    const int i = e * NT + threadIdx.x;
+    if (i < n) lds[i] = AFFINE ? t[e] * a + b : t[e];
+  }
+}
+
+template <int NT, int EPT, int LPT, bool AFFINE, bool STATS>
+__global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
+    const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
+    const float* __restrict__ ypos, const float* __restrict__ scale,
+    const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
+    int Ho, int stride, int add_half) {
+  extern __shared__ float pl[];   // Hb*W staged input (affine applied)
+  __shared__ float red[2 * NT / 64];
+  const int plane = blockIdx.x;
+  const int c = plane % C;
+  float* __restrict__ dst = out + (size_t)plane * Ho * W;
+  const float y = add_half ? ypos[c] + 0.5f : ypos[c];   // shift.py:17-18 (fp32 add)
+  const Geom g = make_geom(xpos[c], y);
+  float a = 1.f, b = 0.f;
+  if (AFFINE) { a = scale[c]; b = shift[c]; }
+  stage_plane<NT, LPT, AFFINE>(in + (size_t)plane * Hb * W, pl, Hb * W, a, b);
+  __syncthreads();
+  const int n = Ho * W;
+  double run_n = 0.0, run_mean = 0.0, run_m2 = 0.0;  // block-uniform (STATS only)
+  for (int base = 0; base < n; base += EPT * NT) {
+    float v[EPT];
+    Walker pos(base + threadIdx.x, NT, W);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      TapIdx ti;
+      tap_idx(pos.h * stride + g.y1, pos.w + g.x1, Hb, W, ti);
+      const float q11 = sel(pl[ti.o00], ti.m00), q21 = sel(pl[ti.o01], ti.m01);
+      const float q12 = sel(pl[ti.o10], ti.m10), q22 = sel(pl[ti.o11], ti.m11);
+      const int o = base + e * NT + threadIdx.x;
+      const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
+      v[e] = o < n ? val : 0.f;
+      if (o < n) dst[o] = val;
+      pos.next();
+    }
+    if (STATS) {
+      const int cnt = min(n - base, EPT * NT);
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) s += v[e];
+      s = block_sum(s, red);
+      const float mean = s / (float)cnt;
+      float m2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        const int o = base + e * NT + threadIdx.x;
+        const float d = v[e] - mean;
+        m2 += (o < n) ? d * d : 0.f;
+      }
+      m2 = block_sum(m2, red);
+      const Moments m = merge({run_n, run_mean, run_m2}, {(double)cnt, (double)mean, (double)m2});
+      run_n = m.n;
+      run_mean = m.mean;
+      run_m2 = m.m2;
+    }
+  }
+  if (STATS && threadIdx.x == 0) pstats[plane] = make_float2((float)run_mean, (float)run_m2);
+}
+
+template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP>
+__global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
+    const float* __restrict__ gout, const float* __restrict__ in,
+    const float* __restrict__ xpos, const float* __restrict__ ypos,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
+    float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
+    int Hb, int W, int Ho, int add_half) {
+  extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input]
+  __shared__ float red[2 * NT / 64];
+  const int plane = blockIdx.x;
+  const int c = plane % C;
+  const int nb = Hb * W, nt = Ho * W;
+  float* gs = lds;
+  float* xs = lds + nt;
+  float bmu = 0.f, bis = 0.f;
+  if (BNP) { bmu = bn_mean[c]; bis = bn_invstd[c]; }
+  const float x = xpos[c];
+  const float y = add_half ? ypos[c] + 0.5f : ypos[c];
+  float a = 1.f, b = 0.f;
+  if (AFFINE) { a = scale[c]; b = shift[c]; }
+  // one staging pass: both planes' loads in flight together (LPT covers nt + nb)
+  {
+    const float* __restrict__ go = gout + (size_t)plane * nt;
+    const float* __restrict__ src = in + (size_t)plane * nb;
+    const int ntot = nt + nb;
+    float t[LPT];
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int i = min(e * NT + (int)threadIdx.x, ntot - 1);
+      t[e] = i < nt ? go[i] : src[i - nt];
+    }
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int i = e * NT + threadIdx.x;
+      if (i < ntot) lds[i] = t[e];
+    }
+  }
+  __syncthreads();
+  float* __restrict__ gi = gin + (size_t)plane * nb;
+
+  // (1) grad_input over the bottom grid (.cu:108-150 stride 1; .cu:191-254 stride 2)
+  float bs0 = 0.f, bs1 = 0.f;
+  {
+    const Geom r = make_geom(-x, -y);
+    Walker pos(threadIdx.x, NT, W);
+    for (int o = threadIdx.x; o < nb; o += NT) {
+      const int h1 = pos.h + r.y1;
+      const int w1 = pos.w + r.x1;
+      TapIdx ti;
+      if (STRIDE == 1) {
+        tap_idx(h1, w1, Ho, W, ti);
+      } else {
+        const int h2 = h1 + 1;
+        const int hq1 = (h1 % 2 == 0) ? h1 / 2 : -1;
+        const int hq2 = (h2 % 2 == 0) ? h2 / 2 : -1;
+        TapIdx t1, t2;
+        tap_idx(hq1, w1, Ho, W, t1);
+        tap_idx(hq2, w1, Ho, W, t2);
+        ti.o00 = t1.o00; ti.o01 = t1.o01; ti.m00 = t1.m00; ti.m01 = t1.m01;
+        ti.o10 = t2.o00; ti.o11 = t2.o01; ti.m10 = t2.m00; ti.m11 = t2.m01;
+      }
+      float val = 0.f;
+      if (nt > 0) {
+        const float q11 = sel(gs[ti.o00], ti.m00), q21 = sel(gs[ti.o01], ti.m01);
+        const float q12 = sel(gs[ti.o10], ti.m10), q22 = sel(gs[ti.o11], ti.m11);
+        val = blend(q11, q21, q12, q22, r.dx, r.dy);
+      }
+      const float rin = xs[o];
+      if (RELU_MASK) val = rin > 0.f ? val : 0.f;
+      gi[o] = val;
+      if (BNP) {
+        bs0 += val;
+        bs1 += val * ((rin - bmu) * bis);
+      }
+      pos.next();
+    }
+  }
+
+  // (2) position gradients over the top grid (.cu:321-349), summed over the plane
+  float ax = 0.f, ay = 0.f;
+  {
+    const Geom g = make_geom(x, y);
+    Walker pos(threadIdx.x, NT, W);
+    for (int o = threadIdx.x; o < nt; o += NT) {
+      TapIdx ti;
+      tap_idx(pos.h * STRIDE + g.y1, pos.w + g.x1, Hb, W, ti);
+      float q11 = xs[ti.o00], q21 = xs[ti.o01], q12 = xs[ti.o10], q22 = xs[ti.o11];
+      if (AFFINE) { q11 = q11 * a + b; q21 = q21 * a + b; q12 = q12 * a + b; q22 = q22 * a + b; }
+      q11 = sel(q11, ti.m00);
+      q21 = sel(q21, ti.m01);
+      q12 = sel(q12, ti.m10);
+      q22 = sel(q22, ti.m11);
+      const float vx = (1.f - g.dy) * (q21 - q11) + g.dy * (q22 - q12);
+      const float vy = (1.f - g.dx) * (q12 - q11) + g.dx * (q22 - q21);
+      const float gg = gs[o];
+      ax += vx * gg;
+      ay += vy * gg;
+      pos.next();
+    }
+  }
+  block_sum2(ax, ay, red);
+  if (threadIdx.x == 0) pgrad[plane] = make_float2(ax, ay);
+  if (BNP) {
+    block_sum2(bs0, bs1, red);
+    if (threadIdx.x == 0) bn_part[plane] = make_float2(bs0, bs1);
+  }
+}
+
 // mean over the batch of the per-plane sums (== mean_b then sum_w, sum_h of .cu:501-509
 // up to rounding), then applyShiftConstraint (.cu:370-395) with its float/double
 // promotions: sqrt(dy*dy) in float (correctly rounded), quotients in float, times the
@@ -362,6 +554,25 @@ void launch_fwd(bool affine, bool stats, const float* in, float* out, const floa
 #undef SGCN_FWD
 }
 
+// LDS path: EPT = LPT (the output plane is never larger than the staged input plane)
+template <int LPT>
+void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const float* xpos,
+                    const float* ypos, const float* scale, const float* shift, float2* ps,
+                    int B, int C, int H, int W, int Ho, int stride, int add_half,
+                    hipStream_t st) {
+  dim3 grid(B * C), block(kThreads);
+  const size_t lds = (size_t)H * W * sizeof(float);
+#define SGCN_FWDL(A, S)                                                                  \
+  tshift_fwd_lds_kernel<kThreads, LPT, LPT, A, S><<<grid, block, lds, st>>>(            \
+      in, out, xpos, ypos, scale, shift, ps, C, H, W, Ho, stride, add_half)
+  if (affine) {
+    if (stats) SGCN_FWDL(true, true); else SGCN_FWDL(true, false);
+  } else {
+    if (stats) SGCN_FWDL(false, true); else SGCN_FWDL(false, false);
+  }
+#undef SGCN_FWDL
+}
+
 template <int EPT, int STRIDE>
 void launch_bwd(bool affine, bool relu, const float* gout, const float* in, const float* xpos,
                 const float* ypos, const float* scale, const float* shift, const float* bmu,
@@ -385,6 +596,40 @@ void launch_bwd(bool affine, bool relu, const float* gout, const float* in, cons
     }
   }
 #undef SGCN_BWD
+}
+
+constexpr int kBwdThreads = 512;
+
+template <int LPT, int STRIDE>
+void launch_bwd_lds(bool affine, bool relu, const float* gout, const float* in,
+                    const float* xpos, const float* ypos, const float* scale,
+                    const float* shift, const float* bmu, const float* bis, float* gin,
+                    float2* pg, float2* bp, int B, int C, int H, int W, int Ho, int add_half,
+                    hipStream_t st) {
+  dim3 grid(B * C), block(kBwdThreads);
+  const size_t lds = (size_t)(H + Ho) * W * sizeof(float);
+#define SGCN_BWDL(A, R, P)                                                                  \
+  tshift_bwd_lds_kernel<kBwdThreads, LPT, A, R, STRIDE, P><<<grid, block, lds, st>>>(      \
+      gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, Ho, add_half)
+  if (bp) {
+    if (affine) {
+      if (relu) SGCN_BWDL(true, true, true); else SGCN_BWDL(true, false, true);
+    } else {
+      if (relu) SGCN_BWDL(false, true, true); else SGCN_BWDL(false, false, true);
+    }
+  } else {
+    if (affine) {
+      if (relu) SGCN_BWDL(true, true, false); else SGCN_BWDL(true, false, false);
+    } else {
+      if (relu) SGCN_BWDL(false, true, false); else SGCN_BWDL(false, false, false);
+    }
+  }
+#undef SGCN_BWDL
+}
+
+int pick_lpt(int n, int nt) {
+  const int per = (n + nt - 1) / nt;
+  return per <= 8 ? 8 : (per <= 16 ? 16 : 32);
 }
 
 int pick_ept(int n) {
@@ -412,6 +657,15 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
   const bool aff = in_scale != nullptr, stats = plane_stats != nullptr;
   float2* ps = (float2*)plane_stats;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
+  if (H * W <= kFwdLdsMax) {
+    switch (pick_lpt(H * W, kThreads)) {
+      case 8: launch_fwd_lds<8>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
+      case 16: launch_fwd_lds<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
+      default: launch_fwd_lds<32>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
+    }
+    SGCN_LAUNCH_CHECK();
+    return 0;
+  }
   switch (pick_ept(Ho * W)) {
     case 8: launch_fwd<8>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
     case 16: launch_fwd<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
@@ -441,6 +695,16 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   float2* pg = (float2*)ws;
   float2* bp = (float2*)bn_part;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
+  if ((H + Ho) * W <= kBwdLdsMax && H > 0) {
+    const int lpt = pick_lpt((H + Ho) * W, kBwdThreads);
+#define SGCN_BWDL_LPT(L)                                                                      \
+  (stride == 1 ? launch_bwd_lds<L, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,  \
+                                      bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st) \
+               : launch_bwd_lds<L, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,  \
+                                      bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st))
+    if (lpt == 8) SGCN_BWDL_LPT(8); else if (lpt == 16) SGCN_BWDL_LPT(16); else SGCN_BWDL_LPT(32);
+#undef SGCN_BWDL_LPT
+  } else {
   const int ept = pick_ept(H * W);
 #define SGCN_BWD_EPT(E)                                                                     \
   (stride == 1 ? launch_bwd<E, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, \
@@ -449,6 +713,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
                                   bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st))
   if (ept == 8) SGCN_BWD_EPT(8); else if (ept == 16) SGCN_BWD_EPT(16); else SGCN_BWD_EPT(32);
 #undef SGCN_BWD_EPT
+  }
   SGCN_LAUNCH_CHECK();
   tshift_pos_finalize_kernel<<<(C + 31) / 32, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();

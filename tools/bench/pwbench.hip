@@ -1,0 +1,157 @@
+// Microbenchmark of the pointwise-contraction kernels on the unit shapes of the NTU
+// model (tuning harness; not part of the product library). Includes the kernel source
+// directly so template variants can be launched side by side; every variant's output is
+// compared bit for bit with the product configuration's.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/bench/pwbench.hip -o tools/bench/pwbench
+#include "../../shift-gcn_amd/csrc/pwconv.hip"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace sgcn;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+struct Shape { const char* name; int B, M, K, T, V; bool mask, rot; };
+
+template <typename F>
+float timeit(F&& launch, hipStream_t st, int reps) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int i = 0; i < 2; ++i) launch();
+  CK(hipEventRecord(e0, st));
+  for (int i = 0; i < reps; ++i) launch();
+  CK(hipEventRecord(e1, st));
+  CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipGetLastError());
+  return ms * 1000.f / reps;
+}
+
+static std::vector<float> g_h1, g_h2;
+bool same(const float* y, const float* y2, size_t n) {
+  g_h1.resize(n); g_h2.resize(n);
+  CK(hipMemcpy(g_h1.data(), y, n * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(g_h2.data(), y2, n * 4, hipMemcpyDeviceToHost));
+  return memcmp(g_h1.data(), g_h2.data(), n * 4) == 0;
+}
+
+template <int BM, int BN, int WM, int WN>
+void dw_variant(const char* name, const Shape& s, DwArgs a, int S, hipStream_t st, float* ws,
+                float* dwref, float* dwout, double fl, double by) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.Nc + BN - 1) / BN);
+  const int N = a.T * a.V;
+  const int total = a.B * ((N + 31) / 32);
+  if (S > total) S = total;
+  if ((size_t)S * a.M * a.Nc * 4 > ((size_t)256 << 20)) { printf("    S=%d: slab too large, skipped\n", S); return; }
+  a.chunks_per_split = (total + S - 1) / S;
+  a.slab = ws;
+  a.bslab = nullptr;
+  dim3 grid(tiles, S);
+  const size_t dyn = s.mask ? (size_t)a.V * BN * 4 : 0;
+  const int MN = a.M * a.Nc;
+  auto L = [&]() {
+    if (s.mask) pw_dw_kernel<BM, BN, WM, WN, true><<<grid, 64 * WM * WN, dyn, st>>>(a);
+    else pw_dw_kernel<BM, BN, WM, WN, false><<<grid, 64 * WM * WN, 0, st>>>(a);
+    slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(a.slab, S, MN, a.M, a.Nc, dwout, 0, 0);
+  };
+  float us = timeit(L, st, 10);
+  printf("%-20s %-26s S=%5d %8.1f us  %6.1f TF/s  %6.2f TB/s  %s\n", s.name, name, S, us,
+         fl / us / 1e6, by / us / 1e6, dwref ? "" : "(ref)");
+  if (dwref) {
+    // different split counts sum in different orders: report max relative difference
+    std::vector<float> h1(MN), h2(MN);
+    CK(hipMemcpy(h1.data(), dwref, MN * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(h2.data(), dwout, MN * 4, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    for (int i = 0; i < MN; ++i) { md = fmax(md, fabs(h1[i] - h2[i])); mx = fmax(mx, fabs(h1[i])); }
+    printf("    max|diff|/max|ref| = %.2e\n", md / mx);
+  }
+}
+
+int main(int argc, char** argv) {
+  const bool do_fwd = argc < 2 || strchr(argv[1], 'f');
+  const bool do_dw = argc < 2 || strchr(argv[1], 'w');
+  Shape shapes[] = {
+    {"l2 tcn 64x64 T300", 128, 64, 64, 300, 25, false, false},
+    {"l2 gcn 64x64 T300", 128, 64, 64, 300, 25, true, true},
+    {"l6 tcn 128 T150", 128, 128, 128, 150, 25, false, false},
+    {"l6 gcn 128 T150", 128, 128, 128, 150, 25, true, true},
+    {"l9 tcn 256 T75", 128, 256, 256, 75, 25, false, false},
+    {"l9 gcn 256 T75", 128, 256, 256, 75, 25, true, true},
+    {"l5 tcn 128 T300", 128, 128, 128, 300, 25, false, false},
+  };
+  hipStream_t st; CK(hipStreamCreate(&st));
+  size_t maxe = (size_t)128 * 128 * 300 * 25;
+  float *x, *y, *y2, *y3, *w, *mask, *ws, *dw1, *dw2;
+  CK(hipMalloc(&x, maxe * 4)); CK(hipMalloc(&y, maxe * 4)); CK(hipMalloc(&y2, maxe * 4)); CK(hipMalloc(&y3, maxe * 4));
+  CK(hipMalloc(&w, 256 * 256 * 4)); CK(hipMalloc(&mask, 64 * 256 * 4));
+  CK(hipMalloc(&ws, 256 << 20)); CK(hipMalloc(&dw1, 256 * 256 * 4)); CK(hipMalloc(&dw2, 256 * 256 * 4));
+  std::vector<float> h(maxe);
+  for (size_t i = 0; i < maxe; ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
+  CK(hipMemcpy(x, h.data(), maxe * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(y, h.data() + 7, maxe * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(w, h.data(), 256 * 256 * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(mask, h.data(), 64 * 256 * 4, hipMemcpyHostToDevice));
+  for (auto& s : shapes) {
+    const long long N = (long long)s.T * s.V;
+    const double P = (double)s.B * N;
+    const double fl = 2.0 * P * s.M * s.K, by = 4.0 * P * (s.M + s.K);
+    if (do_fwd) {
+      FwdArgs a{};
+      a.A = w; a.lda = s.K; a.a_mcontig = 0; a.bias = nullptr;
+      a.x = {x, s.K * N, N, 1, s.rot ? 1 : 0};
+      a.mask = s.mask ? mask : nullptr;
+      a.y = {y2, s.M * N, N, 1, s.rot ? 1 : 0};
+      a.M = s.M; a.K = s.K; a.T = s.T; a.V = s.V; a.B = s.B;
+      auto L = [&]() {
+        sgcn_pw_fwd(w, 0, nullptr, x, s.K * N, N, 1, s.rot ? 1 : 0, s.mask ? mask : nullptr,
+                    y2, s.M * N, N, 1, s.rot ? 1 : 0, 0, 0, s.B, s.M, s.K, s.T, s.V, st);
+      };
+      float us = timeit(L, st, 20);
+      printf("%-20s %-26s %8.1f us  %6.1f TF/s  %6.2f TB/s\n", s.name, "fwd product", us,
+             fl / us / 1e6, by / us / 1e6);
+      FwdArgs a3 = a;
+      a3.y.ptr = y3;
+      a3.x_bytes = plane_bytes(a.x.bstride, a.x.cstride, 1, s.B, s.K, s.T, s.V);
+      a3.y_bytes = plane_bytes(a.y.bstride, a.y.cstride, 1, s.B, s.M, s.T, s.V);
+      a3.a_bytes = s.M * s.K * 4;
+      a3.mask_bytes = s.V * s.K * 4;
+      a3.relu = 0;
+      auto v3 = [&](const char* nm, auto fn) {
+        float u = timeit(fn, st, 20);
+        printf("%-20s %-26s %8.1f us  %6.1f TF/s  %6.2f TB/s   bit-identical: %s\n", s.name, nm, u,
+               fl / u / 1e6, by / u / 1e6, same(y2, y3, (size_t)s.B * s.M * N) ? "yes" : "NO");
+      };
+      if (s.M <= 64) {
+        v3("v3 64x256 w2x4", [&]() { launch_pwg3<64, 256, 2, 4>(a3, false, st); });
+      } else if (s.M <= 128) {
+        v3("v3 128x256 w2x4", [&]() { launch_pwg3<128, 256, 2, 4>(a3, false, st); });
+      } else {
+        v3("v3 256x128 w4x2", [&]() { launch_pwg3<256, 128, 4, 2>(a3, false, st); });
+      }
+    }
+    if (do_dw) {
+      // dW[m][c] = sum_p G(m,p) X(c,p): G = y (M rows), X = x (K rows)
+      DwArgs d{};
+      d.g = {y, s.M * N, N, 1, s.rot ? 1 : 0};
+      d.x = {x, s.K * N, N, 1, s.rot ? 1 : 0};
+      d.mask = s.mask ? mask : nullptr;
+      d.M = s.M; d.Nc = s.K; d.T = s.T; d.V = s.V; d.B = s.B;
+      const int bm = dw_tile(s.M), bn = dw_tile(s.K);
+      const int tiles = ((s.M + bm - 1) / bm) * ((s.K + bn - 1) / bn);
+      const int S0 = dw_splits(s.M, s.K, s.B, (int)N, tiles);
+      if (bm == 128 && bn == 128) {
+        dw_variant<128, 128, 4, 2>("dw 128x128 w4x2", s, d, S0, st, ws, nullptr, dw1, fl, by);
+        for (int S : {512, 1024, 2048}) dw_variant<128, 128, 4, 2>("dw 128x128 w4x2", s, d, S, st, ws, dw1, dw2, fl, by);
+        for (int S : {256, 512, 1024}) dw_variant<128, 128, 2, 2>("dw 128x128 w2x2", s, d, S, st, ws, dw1, dw2, fl, by);
+      } else {
+        dw_variant<64, 64, 2, 2>("dw 64x64 w2x2", s, d, S0, st, ws, nullptr, dw1, fl, by);
+        for (int S : {1024, 2048, 4096}) dw_variant<64, 64, 2, 2>("dw 64x64 w2x2", s, d, S, st, ws, dw1, dw2, fl, by);
+      }
+    }
+  }
+  printf("done\n");
+  return 0;
+}
