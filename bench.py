@@ -40,6 +40,18 @@ CONFIGS = {
 GFLOP_PER_CLIP = {"ntu": 21.416, "mp": 14.134}
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 matrix (= vector) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0      # HBM3E spec
+# HBM bytes per C-ABI call of each op class from the committed rocprofv3 PMC passes
+# (tools/pmc_traffic.sh + tools/pmc_summary.py --json) of this code version
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(op):
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+        return d["ops"][op]["bytes_per_call"], d.get("source", "")
+    except (OSError, KeyError, ValueError):
+        return None, ""
 
 
 def parse():
@@ -196,9 +208,14 @@ def main():
         else:
             achieved = d["bytes"] / d["launches"] / per_launch_s / 1e9
             peak, unit = PEAK_HBM_GBS, "GB/s"
+        traffic, tsrc = pmc_traffic(dom)
         roof = {"bound": "mfma" if mfma else "hbm", "kernel": dom,
                 "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4),
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": tsrc or None,
+                "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
                 "launches_per_step": d["launches"] // max(1, min(args.steps, 5)),
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
                 "step_breakdown_ms": {k: round(v["ms_total"] / max(1, min(args.steps, 5)), 3)

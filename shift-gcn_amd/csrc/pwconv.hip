@@ -327,6 +327,7 @@ struct DwArgs {
   float* bslab;       // optional [S][M] row sums of G
   int M, Nc, T, V, B;
   int chunks_per_split;
+  unsigned g_bytes, x_bytes, mask_bytes;   // buffer ranges (pw_dw3_kernel)
 };
 
 template <int BM, int BN, int WM, int WN, bool MASK>
@@ -482,6 +483,183 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// dW v3: the same split-K contraction with a VALU-lean main loop (see pwg_fwd_kernel).
+// Positions are flattened over (sample, t, v) and cut into chunks of BKP; a lane owns one
+// position of the chunk (its (b, t, v) advanced incrementally, no division in the loop)
+// and RPW = 64/BKP rows per wave instruction; the row offset is a wave-uniform soffset.
+// Positions past the split's end load 0 through the descriptor range.
+// ------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, int BKP, bool MASK, bool GROT, bool XROT, bool BIAS>
+__global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
+  // row pitch: the per-chunk stores put BKP positions x (32/BKP) rows in one 32-lane
+  // ds_write group; a pitch = 2 (mod 32) words (BKP = 16) or odd (BKP = 32) keeps them on
+  // distinct banks. Fragment reads (32 consecutive words per half-wave) never conflict.
+  constexpr int PAD = BKP == 16 ? 34 : 33;
+  constexpr int AP = BM + PAD, BP = BN + PAD;
+  constexpr int RPW = 64 / BKP;            // rows covered by one wave instruction
+  constexpr int RSTEP = NT / BKP;          // rows between a thread's consecutive loads
+  constexpr int G_PER = BM / RSTEP, X_PER = BN / RSTEP;
+  static_assert(MI >= 1 && NJ >= 1 && G_PER >= 1 && X_PER >= 1, "bad tile");
+  static_assert(BM % RSTEP == 0 && BN % RSTEP == 0 && 64 % BKP == 0, "bad tile");
+  __shared__ float As[2][BKP * AP];
+  __shared__ float Bs[2][BKP * BP];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int ntn = (p.Nc + BN - 1) / BN;
+  const int m0 = (blockIdx.x / ntn) * BM, c0 = (blockIdx.x % ntn) * BN;
+  const int split = blockIdx.y;
+  const int V = p.V, T = p.T, N = T * V;
+  const int P = p.B * N;
+  const int nch = (P + BKP - 1) / BKP;
+  const int q_begin = split * p.chunks_per_split;
+  const int q_end = min(q_begin + p.chunks_per_split, nch);
+  const int p_end = min(q_end * BKP, P);
+  const auto gr = make_rsrc(p.g.ptr, p.g_bytes);
+  const auto xr = make_rsrc(p.x.ptr, p.x_bytes);
+  const auto mr = make_rsrc(MASK ? p.mask : p.x.ptr, MASK ? p.mask_bytes : 0u);
+
+  const int kq = lane % BKP;          // position of this lane within a chunk
+  const int rsub = lane / BKP;        // row within the wave instruction
+  const int rw = wid * RPW;           // uniform row base of this wave
+  // lane position state (advanced by BKP per chunk)
+  int pp = q_begin * BKP + kq;
+  int b = pp / N, n = pp - (pp / N) * N;
+  int t = n / V, v = n - (n / V) * V;
+  const int dt = BKP / V, dv = BKP - (BKP / V) * V;
+  const unsigned gcs4 = (unsigned)(p.g.cstride * 4), xcs4 = (unsigned)(p.x.cstride * 4);
+  const int g_step = GROT ? rot_step(RSTEP, p.g.rsign, V) : 0;
+  const int x_step = XROT ? rot_step(RSTEP, p.x.rsign, V) : 0;
+  const int g_rot0 = GROT ? pmod(p.g.rsign * (m0 + rw + rsub), V) : 0;
+  const int x_rot0 = XROT ? pmod(p.x.rsign * (c0 + rw + rsub), V) : 0;
+
+  float ra[G_PER], rb[X_PER], rm[MASK ? X_PER : 1], rsum[BIAS ? G_PER : 1];
+#pragma unroll
+  for (int i = 0; i < (BIAS ? G_PER : 1); ++i) rsum[i] = 0.f;
+
+  auto load_chunk = [&]() {
+    const bool ok = pp < p_end;
+    const unsigned gb = ok ? (unsigned)(((long long)b * p.g.bstride +
+                                         (long long)t * p.g.tstride * V) * 4) : p.g_bytes;
+    const unsigned xb = ok ? (unsigned)(((long long)b * p.x.bstride +
+                                         (long long)t * p.x.tstride * V) * 4) : p.x_bytes;
+    const unsigned lg = (unsigned)rsub * gcs4, lx = (unsigned)rsub * xcs4;
+    int cg = v + g_rot0;
+    cg = cg >= V ? cg - V : cg;
+#pragma unroll
+    for (int i = 0; i < G_PER; ++i) {
+      const unsigned voff = gb + lg + (unsigned)((GROT ? cg : v) * 4);
+      ra[i] = bload(gr, voff, (unsigned)(m0 + rw + i * RSTEP) * gcs4);
+      if (GROT) {
+        cg += g_step;
+        cg = cg >= V ? cg - V : cg;
+      }
+    }
+    int cx = v + x_rot0;
+    cx = cx >= V ? cx - V : cx;
+    const unsigned mcol = (unsigned)((v * p.Nc + rsub) * 4);
+#pragma unroll
+    for (int i = 0; i < X_PER; ++i) {
+      const unsigned voff = xb + lx + (unsigned)((XROT ? cx : v) * 4);
+      rb[i] = bload(xr, voff, (unsigned)(c0 + rw + i * RSTEP) * xcs4);
+      if (MASK) rm[i] = bload(mr, mcol, (unsigned)(c0 + rw + i * RSTEP) * 4u);
+      if (XROT) {
+        cx += x_step;
+        cx = cx >= V ? cx - V : cx;
+      }
+    }
+    // advance this lane's position by one chunk
+    pp += BKP;
+    n += BKP;
+    v += dv;
+    t += dt;
+    if (v >= V) { v -= V; ++t; }
+    while (n >= N) { n -= N; ++b; t -= T; }   // a chunk may exceed a tiny sample (N < BKP)
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < G_PER; ++i) {
+      As[buf][kq * AP + rw + rsub + i * RSTEP] = ra[i];
+      if (BIAS) rsum[i] += ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < X_PER; ++i)
+      Bs[buf][kq * BP + rw + rsub + i * RSTEP] = MASK ? rb[i] * rm[i] : rb[i];
+  };
+
+  f32x16 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
+
+  const int kl = lane >> 5, cl = lane & 31;
+  const int nq = q_end - q_begin;
+  if (nq > 0) {
+    load_chunk();
+    store_chunk(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nq; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nq) load_chunk();
+    const float* __restrict__ Aw = As[cur] + kl * AP + wm * (BM / WM) + cl;
+    const float* __restrict__ Bw = Bs[cur] + kl * BP + wn * (BN / WN) + cl;
+    float af[2][MI], bf[2][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[0][i] = Aw[i * 32];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[0][j] = Bw[j * 32];
+#pragma unroll
+    for (int kk = 0; kk < BKP; kk += 2) {
+      const int c2 = (kk >> 1) & 1;
+      if (kk + 2 < BKP) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[c2 ^ 1][i] = Aw[(kk + 2) * AP + i * 32];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bf[c2 ^ 1][j] = Bw[(kk + 2) * BP + j * 32];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[c2][i], bf[c2][j], acc[i][j],
+                                                           0, 0, 0);
+    }
+    if (s + 1 < nq) store_chunk(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* slab = p.slab + (size_t)split * p.M * p.Nc;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = c0 + wn * (BN / WN) + j * 32 + cl;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        if (m < p.M && c < p.Nc) slab[(size_t)m * p.Nc + c] = acc[i][j][r];
+      }
+  }
+  if (BIAS && (blockIdx.x % ntn) == 0) {
+    // row rw + rsub + i*RSTEP is shared by the BKP lanes with equal rsub
+#pragma unroll
+    for (int i = 0; i < G_PER; ++i) {
+      float sv = rsum[i];
+#pragma unroll
+      for (int o = BKP / 2; o > 0; o >>= 1) sv += __shfl_xor(sv, o, 64);
+      const int m = m0 + rw + rsub + i * RSTEP;
+      if (kq == 0 && m < p.M) p.bslab[(size_t)split * p.M + m] = sv;
+    }
+  }
+}
+
 // out[i] (+)= sum_s slab[s*n + i], i < n, in a FIXED order (deterministic): 64 outputs
 // per block, 4 split-groups of 64 threads each summing every 4th split with 8 loads in
 // flight, then the 4 group sums added in order. transpose: i = m*Nc + c -> out[c*M + m].
@@ -541,6 +719,74 @@ unsigned plane_bytes(long long bstride, long long cstride, int tstride, int B, i
   return (unsigned)(e * 4);
 }
 
+// split count for pw_dw3: ~target workgroups, slab <= 64 MiB, >= 1 chunk per split
+int dw3_splits(int M, int Nc, int P, int bkp, int tiles, int target) {
+  const int nch = (P + bkp - 1) / bkp;
+  int S = (target + tiles - 1) / tiles;
+  const long long cap = (64LL << 20) / (4LL * M * Nc);
+  if (S > cap) S = (int)cap;
+  if (S > nch) S = nch;
+  return S < 1 ? 1 : S;
+}
+
+struct Dw3Cfg {
+  int bm, bn, bkp, target;
+};
+Dw3Cfg dw3_cfg(int M, int Nc) {
+  if (M <= 64 && Nc <= 64) return {64, 64, 32, 2048};
+  if (M <= 128 && Nc <= 64) return {128, 64, 16, 1536};
+  if (M <= 64 && Nc <= 128) return {64, 128, 16, 1536};
+  if (M <= 128 && Nc <= 128) return {128, 128, 16, 1024};
+  if (Nc <= 128) return {256, 128, 16, 512};
+  return {256, 256, 16, 512};
+}
+
+template <int BM, int BN, int WM, int WN, int BKP>
+void launch_dw3_t(const DwArgs& a, int S, int tiles, hipStream_t st) {
+  dim3 grid(tiles, S);
+  const bool mask = a.mask != nullptr, gr = a.g.rsign != 0, xr = a.x.rsign != 0,
+             bias = a.bslab != nullptr;
+#define SGCN_DW3(MS, GR, XR, BI) \
+  pw_dw3_kernel<BM, BN, WM, WN, BKP, MS, GR, XR, BI><<<grid, 64 * WM * WN, 0, st>>>(a)
+#define SGCN_DW3_BI(MS, GR, XR) (bias ? SGCN_DW3(MS, GR, XR, true) : SGCN_DW3(MS, GR, XR, false))
+  if (mask) {
+    if (gr) { if (xr) SGCN_DW3_BI(true, true, true); else SGCN_DW3_BI(true, true, false); }
+    else { if (xr) SGCN_DW3_BI(true, false, true); else SGCN_DW3_BI(true, false, false); }
+  } else {
+    if (gr) { if (xr) SGCN_DW3_BI(false, true, true); else SGCN_DW3_BI(false, true, false); }
+    else { if (xr) SGCN_DW3_BI(false, false, true); else SGCN_DW3_BI(false, false, false); }
+  }
+#undef SGCN_DW3_BI
+#undef SGCN_DW3
+}
+
+// launches pw_dw3 for one dW into the slab workspace; returns the split count used
+int launch_dw3(const DwArgs& a0, hipStream_t st, float* ws, bool bias) {
+  DwArgs a = a0;
+  const Dw3Cfg c = dw3_cfg(a.M, a.Nc);
+  const int tiles = ((a.M + c.bm - 1) / c.bm) * ((a.Nc + c.bn - 1) / c.bn);
+  const int P = a.B * a.T * a.V;
+  const int S = dw3_splits(a.M, a.Nc, P, c.bkp, tiles, c.target);
+  const int nch = (P + c.bkp - 1) / c.bkp;
+  a.chunks_per_split = (nch + S - 1) / S;
+  a.slab = ws;
+  a.bslab = bias ? ws + (size_t)S * a.M * a.Nc : nullptr;
+  if (c.bm == 64 && c.bn == 64) launch_dw3_t<64, 64, 2, 2, 32>(a, S, tiles, st);
+  else if (c.bm == 128 && c.bn == 64) launch_dw3_t<128, 64, 2, 2, 16>(a, S, tiles, st);
+  else if (c.bm == 64 && c.bn == 128) launch_dw3_t<64, 128, 2, 2, 16>(a, S, tiles, st);
+  else if (c.bm == 128) launch_dw3_t<128, 128, 2, 2, 16>(a, S, tiles, st);
+  else if (c.bn == 128) launch_dw3_t<256, 128, 4, 2, 16>(a, S, tiles, st);
+  else launch_dw3_t<256, 256, 4, 2, 16>(a, S, tiles, st);
+  return S;
+}
+
+size_t dw3_ws_bytes(int B, int M, int Nc, int T, int V) {
+  const Dw3Cfg c = dw3_cfg(M, Nc);
+  const int tiles = ((M + c.bm - 1) / c.bm) * ((Nc + c.bn - 1) / c.bn);
+  const int S = dw3_splits(M, Nc, B * T * V, c.bkp, tiles, c.target);
+  return (size_t)S * ((size_t)M * Nc + M) * sizeof(float);
+}
+
 int dw_splits(int M, int Nc, int B, int N, int tiles) {
   // ~512 workgroups (2 per CU at this kernel's register budget); slab <= 16 MiB
   const int total = B * ((N + 31) / 32);
@@ -552,6 +798,10 @@ int dw_splits(int M, int Nc, int B, int N, int tiles) {
 }
 
 int dw_tile(int X) { return X > 64 ? 128 : 64; }
+
+// pw_dw3 measured faster from 128x128 contractions up (tools/bench/pwbench: l5/l6 tcn,
+// l9 tcn/gcn), equal or slower on the 64-wide masked/rotated ones
+bool use_dw3(int M, int Nc) { return (long long)M * Nc >= 128 * 128; }
 
 }  // namespace
 }  // namespace sgcn
@@ -590,7 +840,7 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   a.V = V;
   a.B = B;
   hipStream_t st = (hipStream_t)stream;
-  const bool mk = mask != nullptr, rl = relu != 0, ac = accumulate != 0;
+  const bool rl = relu != 0, ac = accumulate != 0;
   a.x_bytes = plane_bytes(x_bstride, x_cstride, x_tstride, B, K, T, V);
   a.y_bytes = plane_bytes(y_bstride, y_cstride, y_tstride, B, M, T, V);
   a.a_bytes = (unsigned)((long long)M * K * 4);
@@ -604,6 +854,7 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
 }
 
 size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V) {
+  if (use_dw3(M, Nc)) return dw3_ws_bytes(B, M, Nc, T, V);
   const int tiles = ((M + dw_tile(M) - 1) / dw_tile(M)) * ((Nc + dw_tile(Nc) - 1) / dw_tile(Nc));
   const int S = dw_splits(M, Nc, B, T * V, tiles);
   return (size_t)S * ((size_t)M * Nc + M) * sizeof(float);
@@ -619,34 +870,46 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
   SGCN_REQUIRE(!mask || V <= kMaskMaxV);
   SGCN_REQUIRE(ws_bytes >= sgcn_pw_dw_ws_bytes(B, M, Nc, T, V));
   SGCN_REQUIRE(g_cstride * (long long)M < (1LL << 31) && x_cstride * (long long)Nc < (1LL << 31));
-  const int bm = dw_tile(M), bn = dw_tile(Nc);
-  const int tiles = ((M + bm - 1) / bm) * ((Nc + bn - 1) / bn);
-  const int N = T * V;
-  const int S = dw_splits(M, Nc, B, N, tiles);
-  const int total = B * ((N + 31) / 32);
   DwArgs a;
   a.g = {g, g_bstride, g_cstride, g_tstride, g_rsign};
   a.x = {x, x_bstride, x_cstride, x_tstride, x_rsign};
   a.mask = mask;
-  a.slab = (float*)ws;
-  a.bslab = dbias ? (float*)ws + (size_t)S * M * Nc : nullptr;
   a.M = M;
   a.Nc = Nc;
   a.T = T;
   a.V = V;
   a.B = B;
-  a.chunks_per_split = (total + S - 1) / S;
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(tiles, S);
+  int S;
+  if (use_dw3(M, Nc)) {
+    a.g_bytes = plane_bytes(g_bstride, g_cstride, g_tstride, B, M, T, V);
+    a.x_bytes = plane_bytes(x_bstride, x_cstride, x_tstride, B, Nc, T, V);
+    a.mask_bytes = mask ? (unsigned)(V * Nc * 4) : 0u;
+    SGCN_REQUIRE((long long)(B - 1) * g_bstride + (long long)M * g_cstride + (long long)T * g_tstride * V < (1LL << 29));
+    SGCN_REQUIRE((long long)(B - 1) * x_bstride + (long long)Nc * x_cstride + (long long)T * x_tstride * V < (1LL << 29));
+    S = launch_dw3(a, st, (float*)ws, dbias != nullptr);
+    a.slab = (float*)ws;
+    a.bslab = dbias ? (float*)ws + (size_t)S * M * Nc : nullptr;
+  } else {
+    const int bm = dw_tile(M), bn = dw_tile(Nc);
+    const int tiles = ((M + bm - 1) / bm) * ((Nc + bn - 1) / bn);
+    const int N = T * V;
+    S = dw_splits(M, Nc, B, N, tiles);
+    const int total = B * ((N + 31) / 32);
+    a.slab = (float*)ws;
+    a.bslab = dbias ? (float*)ws + (size_t)S * M * Nc : nullptr;
+    a.chunks_per_split = (total + S - 1) / S;
+    dim3 grid(tiles, S);
 #define SGCN_DW(BM_, BN_)                                                                    \
-  (mask ? pw_dw_kernel<BM_, BN_, BM_ / 32, 2, true>                                           \
-              <<<grid, 64 * (BM_ / 32) * 2, (size_t)V * BN_ * sizeof(float), st>>>(a)       \
-        : pw_dw_kernel<BM_, BN_, BM_ / 32, 2, false><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a))
-  if (bm == 128 && bn == 128) SGCN_DW(128, 128);
-  else if (bm == 128) SGCN_DW(128, 64);
-  else if (bn == 128) SGCN_DW(64, 128);
-  else SGCN_DW(64, 64);
+    (mask ? pw_dw_kernel<BM_, BN_, BM_ / 32, 2, true>                                           \
+                <<<grid, 64 * (BM_ / 32) * 2, (size_t)V * BN_ * sizeof(float), st>>>(a)       \
+          : pw_dw_kernel<BM_, BN_, BM_ / 32, 2, false><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a))
+    if (bm == 128 && bn == 128) SGCN_DW(128, 128);
+    else if (bm == 128) SGCN_DW(128, 64);
+    else if (bn == 128) SGCN_DW(64, 128);
+    else SGCN_DW(64, 64);
 #undef SGCN_DW
+  }
   SGCN_LAUNCH_CHECK();
   const int MN = M * Nc;
   slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(a.slab, S, MN, M, Nc, dw, dw_transpose,

@@ -103,6 +103,29 @@ def test_pw_dw_matches_torch(M, Nc, grot, xrot, mask, transpose):
     torch.testing.assert_close(db.double(), G.sum((0, 2, 3)), rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("B,T,V,Nc", [(3, 1, 5, 128), (2, 9, 33, 128), (5, 7, 25, 200)])
+def test_pw_dw_strided_and_tiny_planes(B, T, V, Nc):
+    """Wide contractions (the pw_dw3 path): a temporal-stride-2 X view, samples smaller than
+    one position chunk (T*V < 16), V=33 rotations, ragged channel counts."""
+    from shiftgcn import ops
+    torch.manual_seed(B * 100 + T)
+    M = 128
+    To = T
+    Ti = 2 * T
+    gr = torch.randn(B, M, To, V, device=DEV)
+    x = torch.randn(B, Nc, Ti, V, device=DEV)
+    mk = torch.rand(V, Nc, device=DEV) + 0.5
+    dw = torch.empty(M, Nc, device=DEV)
+    db = torch.empty(M, device=DEV)
+    ops.pw_dw(ops.PlaneView(gr, 1, -1), ops.PlaneView(x, 2, 1), dw, M, Nc, To, V, mask=mk,
+              dbias=db)
+    G = rot_gather(gr.double(), -1)
+    X = rot_gather(x.double()[:, :, ::2], 1) * mk.double().t()[None, :, None, :]
+    torch.testing.assert_close(dw.double(), torch.einsum("bmtv,bctv->mc", G, X),
+                               rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db.double(), G.sum((0, 2, 3)), rtol=1e-5, atol=1e-4)
+
+
 def test_pw_dw_large_split_is_deterministic():
     from shiftgcn import ops
     torch.manual_seed(0)

@@ -112,25 +112,6 @@ int main(int argc, char** argv) {
       float us = timeit(L, st, 20);
       printf("%-20s %-26s %8.1f us  %6.1f TF/s  %6.2f TB/s\n", s.name, "fwd product", us,
              fl / us / 1e6, by / us / 1e6);
-      FwdArgs a3 = a;
-      a3.y.ptr = y3;
-      a3.x_bytes = plane_bytes(a.x.bstride, a.x.cstride, 1, s.B, s.K, s.T, s.V);
-      a3.y_bytes = plane_bytes(a.y.bstride, a.y.cstride, 1, s.B, s.M, s.T, s.V);
-      a3.a_bytes = s.M * s.K * 4;
-      a3.mask_bytes = s.V * s.K * 4;
-      a3.relu = 0;
-      auto v3 = [&](const char* nm, auto fn) {
-        float u = timeit(fn, st, 20);
-        printf("%-20s %-26s %8.1f us  %6.1f TF/s  %6.2f TB/s   bit-identical: %s\n", s.name, nm, u,
-               fl / u / 1e6, by / u / 1e6, same(y2, y3, (size_t)s.B * s.M * N) ? "yes" : "NO");
-      };
-      if (s.M <= 64) {
-        v3("v3 64x256 w2x4", [&]() { launch_pwg3<64, 256, 2, 4>(a3, false, st); });
-      } else if (s.M <= 128) {
-        v3("v3 128x256 w2x4", [&]() { launch_pwg3<128, 256, 2, 4>(a3, false, st); });
-      } else {
-        v3("v3 256x128 w4x2", [&]() { launch_pwg3<256, 128, 4, 2>(a3, false, st); });
-      }
     }
     if (do_dw) {
       // dW[m][c] = sum_p G(m,p) X(c,p): G = y (M rows), X = x (K rows)
@@ -142,14 +123,26 @@ int main(int argc, char** argv) {
       const int bm = dw_tile(s.M), bn = dw_tile(s.K);
       const int tiles = ((s.M + bm - 1) / bm) * ((s.K + bn - 1) / bn);
       const int S0 = dw_splits(s.M, s.K, s.B, (int)N, tiles);
-      if (bm == 128 && bn == 128) {
-        dw_variant<128, 128, 4, 2>("dw 128x128 w4x2", s, d, S0, st, ws, nullptr, dw1, fl, by);
-        for (int S : {512, 1024, 2048}) dw_variant<128, 128, 4, 2>("dw 128x128 w4x2", s, d, S, st, ws, dw1, dw2, fl, by);
-        for (int S : {256, 512, 1024}) dw_variant<128, 128, 2, 2>("dw 128x128 w2x2", s, d, S, st, ws, dw1, dw2, fl, by);
-      } else {
-        dw_variant<64, 64, 2, 2>("dw 64x64 w2x2", s, d, S0, st, ws, nullptr, dw1, fl, by);
-        for (int S : {1024, 2048, 4096}) dw_variant<64, 64, 2, 2>("dw 64x64 w2x2", s, d, S, st, ws, dw1, dw2, fl, by);
-      }
+      if (bm == 128 && bn == 128) dw_variant<128, 128, 4, 2>("dw product 128x128", s, d, S0, st, ws, nullptr, dw1, fl, by);
+      else dw_variant<64, 64, 2, 2>("dw product 64x64", s, d, S0, st, ws, nullptr, dw1, fl, by);
+      DwArgs d3 = d;
+      d3.g_bytes = plane_bytes(d.g.bstride, d.g.cstride, 1, s.B, s.M, s.T, s.V);
+      d3.x_bytes = plane_bytes(d.x.bstride, d.x.cstride, 1, s.B, s.K, s.T, s.V);
+      d3.mask_bytes = s.mask ? (unsigned)(s.V * s.K * 4) : 0u;
+      int S3 = 0;
+      const int MN = s.M * s.K;
+      auto L3 = [&]() {
+        S3 = launch_dw3(d3, st, ws, false);
+        slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(ws, S3, MN, s.M, s.K, dw2, 0, 0);
+      };
+      float us = timeit(L3, st, 10);
+      std::vector<float> h1(MN), h2(MN);
+      CK(hipMemcpy(h1.data(), dw1, MN * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2.data(), dw2, MN * 4, hipMemcpyDeviceToHost));
+      double md = 0, mx = 0;
+      for (int i = 0; i < MN; ++i) { md = fmax(md, fabs(h1[i] - h2[i])); mx = fmax(mx, fabs(h1[i])); }
+      printf("%-20s %-26s S=%5d %8.1f us  %6.1f TF/s  %6.2f TB/s  max|diff|/max|ref| = %.2e\n",
+             s.name, "dw3", S3, us, fl / us / 1e6, by / us / 1e6, md / mx);
     }
   }
   printf("done\n");

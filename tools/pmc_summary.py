@@ -1,6 +1,10 @@
 """Per-kernel HBM traffic from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
-    python tools/pmc_summary.py <pmc_dir> [--match SUBSTR] [--last N]
+    python tools/pmc_summary.py <pmc_dir> [--match SUBSTR] [--json OUT --tag NAME]
+
+--json writes the HBM bytes per C-ABI call of each launch-timer op class (bench.py's
+roofline classes; an op's helper kernels, e.g. pw_dw's slab reduce, count with it),
+which bench.py reports as roofline.traffic for the dominant class.
 
 FETCH_SIZE / WRITE_SIZE are reported in KB per dispatch. gfx950 correction
 (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128-B request of a wide
@@ -32,10 +36,41 @@ def short(n):
     return n[:i] if i > 0 else n
 
 
+# op class (ops.LaunchTimer name) -> (primary kernel prefix, helper kernel prefixes)
+OP_CLASSES = {
+    "pw_fwd": ("pwg_fwd_kernel", ()),
+    "pw_dw": (("pw_dw_kernel", "pw_dw3_kernel"), ("slab_reduce_kernel",)),
+    "tshift_fwd": (("tshift_fwd_kernel", "tshift_fwd_lds_kernel"), ()),
+    "tshift_bwd": (("tshift_bwd_kernel", "tshift_bwd_lds_kernel"), ("tshift_pos_finalize_kernel",)),
+}
+
+
+def op_traffic(f, w):
+    """{op: {calls, fetch_bytes, write_bytes, bytes_per_call}} over the whole run."""
+    out = {}
+    for op, (prim, helpers) in OP_CLASSES.items():
+        prim = prim if isinstance(prim, tuple) else (prim,)
+        calls, fb, wb = 0, 0.0, 0.0
+        for (n, _, fv, _), (_, _, wv, _) in zip(f, w):
+            k = short(n)
+            if k.startswith(prim):
+                calls += 1
+            elif not k.startswith(helpers):
+                continue
+            fb += 2 * fv
+            wb += wv
+        if calls:
+            out[op] = {"calls": calls, "fetch_bytes_x2": fb / calls, "write_bytes": wb / calls,
+                       "bytes_per_call": (fb + wb) / calls}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--match", default="")
+    ap.add_argument("--json", default="")
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
     f = read(os.path.join(a.dir, "FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
     w = read(os.path.join(a.dir, "WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -50,6 +85,18 @@ def main():
     print(f"{'kernel':70s} {'grid':>9s} {'n':>4s} {'fetchx2 MB':>11s} {'write MB':>9s}")
     for (n, g), (c, fb, wb) in agg.items():
         print(f"{n[:70]:70s} {g:>9s} {c:4d} {2 * fb / c / 1e6:11.1f} {wb / c / 1e6:9.1f}")
+    if a.json:
+        import json
+        ops = op_traffic(f, w)
+        with open(a.json, "w") as fh:
+            json.dump({"source": a.tag or a.dir,
+                       "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate "
+                                 "kernel-trace passes over bench.py --steps 2 --warmup 1; "
+                                 "FETCH_SIZE doubled (gfx950 wide-read correction), WRITE_SIZE "
+                                 "as is (MI355X_MICROARCH.md HBM section); per C-ABI call",
+                       "ops": ops}, fh, indent=1)
+        for k, v in ops.items():
+            print(f"{k:12s} calls={v['calls']:4d} bytes/call={v['bytes_per_call'] / 1e6:9.1f} MB")
 
 
 if __name__ == "__main__":
