@@ -6,7 +6,9 @@ per GPU: Model forward (10 fused TCN_GCN_units on the HIP path), CrossEntropy, b
 [RCCL gradient all-reduce for N>1], SGD(momentum 0.9, nesterov, per-param weight decay).
 Inputs are resident in HBM before the timed region. Weak scaling: 64 clips per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ntu|mp] [--graph 0|1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ntu|mp|ens] [--graph 0|1]
+--config ens: BASELINE config 4 instead (4-stream MediaPipe ensemble inference, bs=256,
+eval mode, one hipGraph per batch): windows/s, its own JSON line.
 N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0 (value = whole-job clips/s), with:
@@ -38,6 +40,7 @@ CONFIGS = {
 }
 # algorithmic fwd+bwd GFLOP per clip (torch FlopCounter on the reference model)
 GFLOP_PER_CLIP = {"ntu": 21.416, "mp": 14.134}
+GFLOP_PER_WINDOW_ENS = 18.85   # 4 MediaPipe forwards per window
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 matrix (= vector) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0      # HBM3E spec
 # HBM bytes per C-ABI call of each op class from the committed rocprofv3 PMC passes
@@ -59,9 +62,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="clips per GPU")
-    ap.add_argument("--config", default="ntu", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None,
+                    help="clips (windows for --config ens) per GPU; default 64 (ens: 256)")
+    ap.add_argument("--config", default="ntu", choices=sorted(CONFIGS) + ["ens"])
     ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph")
+    ap.add_argument("--graph-ens", type=int, default=1,
+                    help="--config ens: replay the ensemble forward as one hipGraph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--roofline", type=int, default=1)
     return ap.parse_args()
@@ -132,6 +138,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if args.config == "ens":
+        return bench_ensemble(args, dev, rank, world, distributed)
+    if args.batch is None:
+        args.batch = 64
 
     import shiftgcn
     from shiftgcn import ops, train
@@ -251,6 +261,118 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+def _roofline(summ, n_iters, value_per_gpu, gflop_per_unit):
+    dom = max(summ, key=lambda k: summ[k]["ms_total"])
+    d = summ[dom]
+    mfma = d["flops"] > 0
+    per_launch_s = d["ms_total"] / d["launches"] / 1e3
+    if mfma:
+        achieved = d["flops"] / d["launches"] / per_launch_s / 1e12
+        peak, unit = PEAK_FP32_TFLOPS, "TFLOP/s"
+    else:
+        achieved = d["bytes"] / d["launches"] / per_launch_s / 1e9
+        peak, unit = PEAK_HBM_GBS, "GB/s"
+    return {"bound": "mfma" if mfma else "hbm", "kernel": dom,
+            "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": None,
+            "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
+            "launches_per_iter": d["launches"] // n_iters,
+            "avg_launch_us": round(per_launch_s * 1e6, 2),
+            "iter_breakdown_ms": {k: round(v["ms_total"] / n_iters, 3)
+                                  for k, v in sorted(summ.items())},
+            "whole_iter_frac_of_fp32_peak": round(
+                value_per_gpu * gflop_per_unit / 1e3 / PEAK_FP32_TFLOPS, 4)}
+
+
+def cpu_baseline_ensemble(seconds_budget=30.0):
+    """The oracle ensemble (reference semantics: batch-1 forwards per window and stream,
+    PyTorch eager on the host cores) on a bounded sample of 2 windows."""
+    from oracle import ensemble_oracle as eo
+    from oracle import model_oracle as mo
+    from shiftgcn.ensemble import MEDIAPIPE_BONE_PAIRS
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch.manual_seed(1)
+        models = {s: mo.Model(num_class=2, num_point=33, num_person=1, graph="unused").eval()
+                  for s in eo.MODALITIES}
+        g = torch.Generator().manual_seed(0)
+        wins = [torch.randn(3, 300, 33, 1, generator=g).numpy() for _ in range(2)]
+        eo.run_ensemble_inference(wins[:1], models, (0.6, 0.6, 0.4, 0.4), MEDIAPIPE_BONE_PAIRS)
+        t0 = time.perf_counter()
+        eo.run_ensemble_inference(wins, models, (0.6, 0.6, 0.4, 0.4), MEDIAPIPE_BONE_PAIRS)
+        dt = time.perf_counter() - t0
+        return {"value": round(len(wins) / dt, 4), "unit": "windows/s", "cores": threads,
+                "kind": "port",
+                "sample": f"2 MediaPipe windows (3,300,33,1), 4 streams, batch-1 forwards "
+                          f"as inference_pipeline.py:355-366, {dt:.2f} s"}
+    finally:
+        torch.set_num_threads(prev)
+
+
+def bench_ensemble(args, dev, rank, world, distributed):
+    """BASELINE config 4: 4-stream (joint/bone/joint-motion/bone-motion) MediaPipe
+    ensemble inference at bs=256 windows per GPU, eval mode, one hipGraph replay per
+    batch. Replicas only across GPUs (inference has no exchange step)."""
+    import shiftgcn
+    from shiftgcn import ops
+    from shiftgcn.ensemble import Ensemble, EnsembleGraph
+    batch = args.batch or 256
+    torch.manual_seed(1)
+    models = [shiftgcn.Model(num_class=2, num_point=33, num_person=1,
+                             graph="graph.mediapipe_pose.Graph").to(dev).eval()
+              for _ in range(4)]
+    ens = Ensemble(models).to(dev)
+    gen = torch.Generator().manual_seed(2000 + rank)
+    x = torch.randn(batch, 3, 300, 33, 1, generator=gen).to(dev)
+    runner = (lambda: ens(x)) if not args.graph_ens else EnsembleGraph(ens, x.shape, dev).run
+    call = (lambda: runner()) if not args.graph_ens else (lambda: runner(x))
+    for _ in range(args.warmup):
+        call()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        call()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = batch * world * args.steps / elapsed
+    roof = None
+    if args.roofline and rank == 0:
+        timer = ops.LaunchTimer()
+        ops.set_launch_timer(timer)
+        n = 3
+        for _ in range(n):
+            ens(x)
+        torch.cuda.synchronize()
+        ops.set_launch_timer(None)
+        roof = _roofline(timer.summary(), n, value / world, GFLOP_PER_WINDOW_ENS)
+    cpu = cpu_baseline_ensemble() if (args.cpu_baseline and rank == 0 and world == 1) else None
+    if rank == 0:
+        print(json.dumps({
+            "metric": "ensemble windows/sec, MediaPipe 4-stream (3,300,33,1) bs=256 inference",
+            "value": round(value, 2), "unit": "windows/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic N(0,1) windows, random-init weights (seeded)",
+            "config": {"workload": f"ENS 4-stream eval forward + score fusion, "
+                                   f"x=({batch},3,300,33,1) per GPU",
+                       "global_batch": batch * world, "per_gpu_batch": batch,
+                       "parallelism": f"replicas{world}", "hipgraph": bool(args.graph_ens)},
+            "roofline": roof, "cpu_baseline": cpu}), flush=True)
     if distributed:
         dist.destroy_process_group()
 

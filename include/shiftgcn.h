@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 5
+#define SGCN_ABI_VERSION 6
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -183,6 +183,25 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
 /* dmask[u][c] (+)= (sum_b dmask_part[b][c][u]) * (1 - tanh(mask[u][c])^2). */
 int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,
                             float* dmask, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Ensemble head (config 4: 4-stream joint/bone/joint-motion/bone-motion inference)
+ * ---------------------------------------------------------------------------------- */
+/* Replaces `derive_modalities(joint_window)` (inference_pipeline.py:284-309) for a whole
+ * batch, fused with Model.forward's head (shift_gcn.py:194-198) when scale/shift given.
+ * joint : (N, C, T, V, M) clip batch;  parent: (V) int32 parent joint of each joint
+ *   (BONE_PAIRS, inference_pipeline.py:16-22; joint 0 is its own parent -> bone 0).
+ * out_* : any subset may be NULL.  bone = joint[v] - joint[parent[v]];
+ *   *_motion[t] = x[t+1] - x[t] for t < T-1, 0 at t = T-1 (bone_motion = bone[t+1] -
+ *   bone[t] evaluated in that order, so the fp32 results are bit-exact).
+ * planes = 0: outputs in the input's (N, C, T, V, M) layout (scale/shift must be NULL);
+ * planes = 1: outputs in the model's (N*M, C, T, V) plane layout, and when scale/shift
+ *   ([4][M*V*C], data_bn eval coefficients of the four models, feature m*V*C + v*C + c)
+ *   are given, data_bn is applied too, so the result feeds l1 directly. */
+int sgcn_modalities(const float* joint, const int* parent, float* out_joint, float* out_bone,
+                    float* out_joint_motion, float* out_bone_motion, const float* scale,
+                    const float* shift, int planes, int N, int C, int T, int V, int M,
+                    void* stream);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -173,6 +173,7 @@ class Model(nn.Module):
             Graph = graph
         self.graph = Graph(**graph_args)
         A = self.graph.A
+        self.num_person, self.in_channels = num_person, in_channels
         self.data_bn = nn.BatchNorm1d(num_person * in_channels * num_point)
         self.l1 = TCN_GCN_unit(3, 64, A, residual=False, num_point=num_point)
         self.l2 = TCN_GCN_unit(64, 64, A, num_point=num_point)
@@ -193,6 +194,11 @@ class Model(nn.Module):
         x = x.permute(0, 4, 3, 1, 2).contiguous().view(N, M * V * C, T)
         x = self.data_bn(x)
         x = x.view(N, M, V, C, T).permute(0, 1, 3, 4, 2).contiguous().view(N * M, C, T, V)
+        return self.forward_planes(x, N, M)
+
+    def forward_planes(self, x, N, M):
+        """Body + head of ``forward`` (shift_gcn.py:200-216) on an input already permuted
+        to (N*M, C, T, V) and normalised by ``data_bn`` (e.g. by ``sgcn_modalities``)."""
         for k in range(1, 11):
             x = getattr(self, f"l{k}")(x)
         c_new = x.size(1)

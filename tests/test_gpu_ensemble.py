@@ -1,0 +1,93 @@
+"""GPU parity of the ensemble path (BASELINE config 4): the fused modality/head kernel
+(bit-exact streams; data_bn within fp32 rounding) and the batched 4-model ensemble, eager
+and hipGraph-replayed, against the oracle and the reference's own fused scores
+(tests/golden/ensemble_fixtures.npz)."""
+import numpy as np
+import pytest
+import torch
+
+import formula
+from oracle import ensemble_oracle as eo
+from test_oracle_ensemble import STREAMS, oracle_models
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("N,T,V,M", [(5, 37, 33, 1), (3, 20, 25, 2), (1, 1, 33, 1),
+                                     (0, 8, 33, 1)])
+def test_modalities_bit_exact(N, T, V, M):
+    from shiftgcn import ensemble as ens
+    pairs = ens.MEDIAPIPE_BONE_PAIRS if V == 33 else ens.NTU_BONE_PAIRS
+    joint = formula.tensor((N, 3, T, V, M), 11 + N + V, 1.0)
+    parent = torch.from_numpy(ens.parent_table(pairs, V)).to(DEV)
+    ref = eo.derive_modalities(joint.numpy(), pairs)
+    got = ens.derive_modalities(joint.to(DEV), parent, planes=False)
+    gotp = ens.derive_modalities(joint.to(DEV), parent, planes=True)
+    for s, g, gp in zip(STREAMS, got, gotp):
+        assert np.array_equal(g.cpu().numpy(), ref[s]), s
+        planes = ref[s].transpose(0, 4, 1, 2, 3).reshape(N * M, 3, T, V)
+        assert np.array_equal(gp.cpu().numpy(), planes), s
+
+
+def test_modalities_with_data_bn_head():
+    """planes + data_bn == the Model.forward head (permute, BatchNorm1d eval, permute)."""
+    import shiftgcn
+    from shiftgcn import ensemble as ens
+    N, T, V, M = 4, 16, 25, 2
+    models = []
+    for k in range(4):
+        m = shiftgcn.Model(num_class=60, num_point=V, num_person=M,
+                           graph="graph.ntu_rgb_d.Graph")
+        formula.fill_state(m, seed=31 + k)
+        models.append(m.to(DEV).eval())
+    e = ens.Ensemble(models, bone_pairs=ens.NTU_BONE_PAIRS).to(DEV)
+    joint = formula.tensor((N, 3, T, V, M), 77, 1.0).to(DEV)
+    streams = ens.derive_modalities(joint, e.parent, planes=True, data_bn=e._data_bn_coef())
+    raw = ens.derive_modalities(joint, e.parent, planes=False)
+    for m, xs, xr in zip(models, streams, raw):
+        with torch.no_grad():
+            x = xr.permute(0, 4, 3, 1, 2).contiguous().view(N, M * V * 3, T)
+            x = m.data_bn(x).view(N, M, V, 3, T).permute(0, 1, 3, 4, 2).reshape(N * M, 3, T, V)
+        err = (xs - x).abs().max().item()
+        assert err <= 2e-6 * max(1.0, x.abs().max().item()), err
+
+
+def _our_ensemble():
+    import shiftgcn
+    from shiftgcn import ensemble as ens
+    models = []
+    for k in range(4):
+        m = shiftgcn.Model(num_class=2, num_point=33, num_person=1,
+                           graph="graph.mediapipe_pose.Graph")
+        formula.fill_state(m, seed=701 + 13 * k)
+        models.append(m.to(DEV).eval())
+    return ens.Ensemble(models).to(DEV)
+
+
+def test_ensemble_matches_reference_scores(golden):
+    fx = golden("ensemble_fixtures.npz")
+    e = _our_ensemble()
+    wins = torch.from_numpy(fx["ens_windows"]).to(DEV)        # (W, 3, T, 33, 1)
+    scores, fused = e(wins)
+    assert np.abs(scores.cpu().numpy() - fx["ens_scores"]).max() < 1e-5
+    ref_fused = sum(np.float32(a) * fx[f"ens_logits_{s}"] for a, s in
+                    zip(fx["weights"], STREAMS))
+    assert np.abs(fused.cpu().numpy() - ref_fused).max() < 1e-4
+    # the batch is computed as one: each window alone gives the same scores
+    s0, _ = e(wins[1:2])
+    assert abs(float(s0[0]) - float(scores[1])) < 1e-6
+
+
+def test_ensemble_graph_replay_matches_eager():
+    e = _our_ensemble()
+    N, T = 6, 48
+    from shiftgcn.ensemble import EnsembleGraph
+    x1 = formula.tensor((N, 3, T, 33, 1), 901, 1.0).to(DEV)
+    x2 = formula.tensor((N, 3, T, 33, 1), 902, 1.0).to(DEV)
+    ens_graph = EnsembleGraph(e, x1.shape, DEV)
+    for x in (x1, x2, x1):
+        s_eager, l_eager = e(x)
+        s_g, l_g = ens_graph.run(x)
+        torch.cuda.synchronize()
+        assert torch.equal(s_g, s_eager) and torch.equal(l_g, l_eager)
