@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 6
+#define SGCN_ABI_VERSION 7
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -140,10 +140,13 @@ int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
 /* y = act(x*scale[f] + shift[f] + res), res = r*rscale[c] + rshift[c] (both given),
  * r (rscale NULL) or 0 (r NULL); act = ReLU if relu. y_stats (optional, B*C float2):
  * per-plane {mean, M2} of y, i.e. the sgcn_moments() partials of the NEXT BatchNorm2d's
- * input, produced without another read of y. */
+ * input, produced without another read of y. gather_m + y_gathered (optional, both or
+ * neither, exclusive with y_stats): also write y_gathered = sgcn_gcn_gather(y, gather_m),
+ * the next unit's Shift_gcn input gathered and masked, from the same registers. */
 int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
                   const float* r, const float* rscale, const float* rshift, int relu,
-                  float* y, float* y_stats, int B, int C, int T, int V, void* stream);
+                  float* y, float* y_stats, const float* gather_m, float* y_gathered, int B,
+                  int C, int T, int V, void* stream);
 
 /* Backward partials: g = dy * (relu ? y > 0 : 1); part[b][f] = {sum g, sum g*xhat};
  * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none).
@@ -164,7 +167,9 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
                          float* coef, void* stream);
 
 /* dx = k1*g + k2*x + k3; dr = g (rcoef NULL, dr given) or rk1*g + rk2*r + rk3;
- * dy_coef as in sgcn_bn_bwd_reduce. */
+ * dy_coef as in sgcn_bn_bwd_reduce. per_joint = 2: per-joint coefficients AND dx written
+ * in the gathered layout dx[b,c,t,(v - c) mod V] (Shift_gcn's shift_out transposed,
+ * shift_gcn.py:114-118,136), so the following contractions read it without rotation. */
 int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
                       const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
@@ -172,6 +177,12 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
 
 /* m = tanh(Feature_Mask) + 1 (shift_gcn.py:129); n = V*C. */
 int sgcn_mask_prep(const float* mask, float* m, int n, void* stream);
+
+/* xg[b,c,t,u] = x0[b,c,t,(u + c) mod V] * m[u*C + c]: Shift_gcn's shift_in gather and
+ * feature mask (shift_gcn.py:125-129; m = tanh(Feature_Mask) + 1 from sgcn_mask_prep),
+ * materialised once per forward for the contraction and its weight gradient. */
+int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, int T, int V,
+                    void* stream);
 
 /* Shift_gcn input side of the backward: dx[b,c,t,v] = dxt[b,c,t,u]*m[u][c] + add1 + add2
  * with u = (v - c) mod V (transpose of the shift_in gather); dmask_part[b][c][u] =

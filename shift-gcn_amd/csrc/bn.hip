@@ -179,14 +179,28 @@ __global__ void bn_eval_coef_kernel(int F, int perm_V, const float* __restrict__
 // ------------------------------------------------------------------------------------
 // OUT_STATS: also write the per-plane {mean, M2} of y (moments of the NEXT BatchNorm's
 // input, shifted by the plane's first output), saving a separate read pass of y.
-template <bool PER_JOINT, int RES, bool RELU, bool OUT_STATS>
+// OUTX = 2 instead: also write yg = the NEXT Shift_gcn's gathered, masked input
+// yg[c,t,(v - c) mod V] = y[c,t,v] * gm[((v - c) mod V)*C + c] (what sgcn_gcn_gather would
+// make from y), saving that kernel's read of y.
+template <bool PER_JOINT, int RES, bool RELU, int OUTX>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     const float* __restrict__ x, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ r,
     const float* __restrict__ rscale, const float* __restrict__ rshift,
-    float* __restrict__ y, float2* __restrict__ ystats, int C, int T, int V) {
+    float* __restrict__ y, float2* __restrict__ ystats, const float* __restrict__ gm,
+    float* __restrict__ yg, int C, int T, int V) {
+  constexpr bool OUT_STATS = OUTX == 1, OUT_G = OUTX == 2;
   __shared__ float red[2 * kThreads / 64];
+  __shared__ float gm_s[OUT_G ? kThreads : 1];   // this channel's mask column, by joint
   const int plane = blockIdx.x, c = plane % C;
+  const int rc = c % V;
+  __shared__ float sc_s[PER_JOINT ? kThreads : 1], sh_s[PER_JOINT ? kThreads : 1];
+  if (OUT_G && (int)threadIdx.x < V) gm_s[threadIdx.x] = gm[threadIdx.x * C + c];
+  if (PER_JOINT && (int)threadIdx.x < V) {
+    sc_s[threadIdx.x] = scale[c * V + threadIdx.x];
+    sh_s[threadIdx.x] = shift[c * V + threadIdx.x];
+  }
+  if (OUT_G || PER_JOINT) __syncthreads();
   const int P = T * V;
   const size_t off = (size_t)plane * P;
   float sc = 0.f, sh = 0.f, rsc = 1.f, rsh = 0.f;
@@ -216,12 +230,17 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     for (int u = 0; u < kU; ++u) {
       const int o = base + u * kThreads + threadIdx.x;
       float a = xv[u];
-      if (PER_JOINT) a = a * scale[c * V + v] + shift[c * V + v];
+      if (PER_JOINT) a = a * sc_s[v] + sh_s[v];
       else a = a * sc + sh;
       if (RES == 1) a += rv[u];
       if (RES == 2) a += rv[u] * rsc + rsh;
       if (RELU) a = fmaxf(a, 0.f);
       if (o < P) y[off + o] = a;
+      if (OUT_G) {
+        int u2 = v - rc;
+        u2 = u2 < 0 ? u2 + V : u2;
+        if (o < P) yg[off + o - v + u2] = a * gm_s[u2];
+      }
       if (OUT_STATS) {
         const float d = o < P ? a - k0 : 0.f;
         s1 += d;
@@ -358,15 +377,30 @@ __global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
 }
 
 // dx = k1[f]*g + k2[f]*x + k3[f]; RES: 1 -> dr = g, 2 -> dr = rk1*g + rk2*r + rk3
-template <bool PER_JOINT, bool RELU, int RES, bool DYT>
+// PJM: 0 per-channel, 1 per-joint, 2 per-joint with dx stored GATHERED: element (c, t, v)
+// goes to (c, t, (v - c) mod V), i.e. the shift_out gather of the next contraction
+// (shift_gcn.py:114-118,136 transposed) is done by this store, not by every GEMM load.
+template <int PJM, bool RELU, int RES, bool DYT>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ coef, int F, const float* __restrict__ r,
     const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
     float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V) {
+  constexpr bool PER_JOINT = PJM != 0, GATH = PJM == 2;
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
   const size_t off = (size_t)plane * P;
+  const int rc = c % V;
+  __shared__ float k_s[PER_JOINT ? 3 * kThreads : 1];   // per-joint {k1, k2, k3} of channel c
+  if (PER_JOINT) {
+    if ((int)threadIdx.x < V) {
+      const int f = c * V + threadIdx.x;
+      k_s[threadIdx.x] = coef[f];
+      k_s[kThreads + threadIdx.x] = coef[F + f];
+      k_s[2 * kThreads + threadIdx.x] = coef[2 * F + f];
+    }
+    __syncthreads();
+  }
   float k1 = 0.f, k2 = 0.f, k3 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
   float d1 = 1.f, d2 = 0.f, d3 = 0.f;
   if (DYT) { d1 = dyc[c]; d2 = dyc[C + c]; d3 = dyc[2 * C + c]; }
@@ -390,18 +424,62 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
       float g = gv[u];
       if (DYT) g = d1 * g + d2 * yv[u] + d3;
       if (RELU) g = yv[u] > 0.f ? g : 0.f;
-      if (PER_JOINT) {
-        const int f = c * V + v;
-        k1 = coef[f]; k2 = coef[F + f]; k3 = coef[2 * F + f];
-      }
+      if (PER_JOINT) { k1 = k_s[v]; k2 = k_s[kThreads + v]; k3 = k_s[2 * kThreads + v]; }
       if (o < P) {
-        dx[off + o] = k1 * g + k2 * xv[u] + k3;
+        int od = o;
+        if (GATH) {
+          const int w = v - rc;
+          od = o - v + (w < 0 ? w + V : w);
+        }
+        dx[off + od] = k1 * g + k2 * xv[u] + k3;
         if (RES == 1) dr[off + o] = g;
         if (RES == 2) dr[off + o] = q1 * g + q2 * rv[u] + q3;
       }
       v += dv;
       if (v >= V) v -= V;
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Shift_gcn input side, forward: shift_in gather + feature mask, materialised once
+// ------------------------------------------------------------------------------------
+// xg[b,c,t,u] = x0[b,c,t,(u + c) mod V] * m[u][c]   (shift_gcn.py:125-129: index_select
+// with shift_in, then * (tanh(Feature_Mask) + 1)). The same fp32 product the contraction
+// loaders would form per element; read by the forward contraction and the weight
+// gradient as a plain plane (no per-element rotation / mask loads in their main loops).
+__global__ __launch_bounds__(kThreads) void gcn_gather_kernel(const float* __restrict__ x0,
+                                                              const float* __restrict__ m,
+                                                              float* __restrict__ xg, int C,
+                                                              int T, int V) {
+  __shared__ float m_s[kThreads];   // this channel's mask column, by joint
+  const int plane = blockIdx.x, c = plane % C;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  const int rc = c % V;
+  if ((int)threadIdx.x < V) m_s[threadIdx.x] = m[threadIdx.x * C + c];
+  __syncthreads();
+  const int dv = kThreads % V;
+  int w = threadIdx.x % V;
+  for (int base = 0; base < P; base += kThreads * kU) {
+    float xv[kU], mv[kU];
+    int ww = w;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int oraw = base + u * kThreads + (int)threadIdx.x;
+      int src = ww + rc;
+      src = src >= V ? src - V : src;
+      xv[u] = x0[off + min(oraw - ww + src, P - 1)];
+      mv[u] = m_s[ww];
+      ww += dv;
+      if (ww >= V) ww -= V;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int o = base + u * kThreads + (int)threadIdx.x;
+      if (o < P) xg[off + o] = xv[u] * mv[u];
+    }
+    w = ww;
   }
 }
 
@@ -415,68 +493,50 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
     const float* __restrict__ dxt, const float* __restrict__ x0, const float* __restrict__ m,
     const float* __restrict__ add1, const float* __restrict__ add2, float* __restrict__ dx,
     float* __restrict__ dmask_part, int C, int T, int V) {
+  // One pass: thread i owns destination joint v' = i % V of rows t = i / V (mod G), so its
+  // source joint u = (v' - c) mod V is fixed: one mask value, one dmask accumulator, and
+  // the x0 factor of the mask gradient, x0[t, (u + c) mod V] = x0[t, v'], is the element
+  // at the thread's own destination address (read once, with add1/add2).
   __shared__ float s0[kThreads];
   const int plane = blockIdx.x, c = plane % C;
-  const int P = T * V;
-  const size_t off = (size_t)plane * P;
+  const size_t off = (size_t)plane * T * V;
   const int rc = c % V;
   const int i = threadIdx.x;
-  // scatter pass over destination positions v' (each thread keeps v' = o mod V)
-  {
-    const int dv = kThreads % V;
-    int v = i % V;
-    for (int base = 0; base < P; base += kThreads * kU) {
-      float gv[kU], a1[kU], a2[kU];
-      int uu[kU];
-      int vv = v;
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int oraw = base + u * kThreads + i;
-        const int o = min(oraw, P - 1);
-        int uq = vv - rc;
-        uq = uq < 0 ? uq + V : uq;
-        uu[u] = uq;
-        gv[u] = dxt[off + min(oraw - vv + uq, P - 1)];
-        if (ADD1) a1[u] = add1[off + o];
-        if (ADD2) a2[u] = add2[off + o];
-        vv += dv;
-        if (vv >= V) vv -= V;
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int o = base + u * kThreads + i;
-        float val = gv[u] * m[uu[u] * C + c];
-        if (ADD1) val += a1[u];
-        if (ADD2) val += a2[u];
-        if (o < P) dx[off + o] = val;
-      }
-      v = vv;
-    }
-  }
-  // mask-gradient partials per u over t
   const int G = kThreads / V;
+  const int vd = i % V, rr = i / V;
+  int us = vd - rc;
+  us = us < 0 ? us + V : us;
+  const float mu = m[us * C + c];
   float acc = 0.f;
   if (i < G * V) {
-    const int u = i % V, rr = i / V;
-    int xv = u + rc;
-    xv = xv >= V ? xv - V : xv;
     for (int t0 = rr; t0 < T; t0 += G * kU) {
-      float gv[kU], xq[kU];
+      float gv[kU], xq[kU], a1[kU], a2[kU];
 #pragma unroll
       for (int k = 0; k < kU; ++k) {
-        const int t = min(t0 + k * G, T - 1);
-        gv[k] = dxt[off + t * V + u];
-        xq[k] = x0[off + t * V + xv];
+        const int row = min(t0 + k * G, T - 1) * V;
+        gv[k] = dxt[off + row + us];
+        xq[k] = x0[off + row + vd];
+        if (ADD1) a1[k] = add1[off + row + vd];
+        if (ADD2) a2[k] = add2[off + row + vd];
       }
 #pragma unroll
-      for (int k = 0; k < kU; ++k) acc += (t0 + k * G < T) ? gv[k] * xq[k] : 0.f;
+      for (int k = 0; k < kU; ++k) {
+        const int t = t0 + k * G;
+        float val = gv[k] * mu;
+        if (ADD1) val += a1[k];
+        if (ADD2) val += a2[k];
+        if (t < T) dx[off + t * V + vd] = val;
+        acc += (t < T) ? gv[k] * xq[k] : 0.f;
+      }
     }
   }
   s0[i] = acc;
   __syncthreads();
-  if (i < V) {
+  if (i < V) {   // partial of source joint u = i: its threads have v' = (i + c) mod V
+    int vq = i + rc;
+    vq = vq >= V ? vq - V : vq;
     float sum = 0.f;
-    for (int g = 0; g < G; ++g) sum += s0[g * V + i];
+    for (int g = 0; g < G; ++g) sum += s0[g * V + vq];
     dmask_part[(size_t)plane * V + i] = sum;
   }
 }
@@ -564,26 +624,31 @@ int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
 
 int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
                   const float* r, const float* rscale, const float* rshift, int relu,
-                  float* y, float* y_stats, int B, int C, int T, int V, void* stream) {
+                  float* y, float* y_stats, const float* gather_m, float* y_gathered, int B,
+                  int C, int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(x && scale && shift && y);
+  SGCN_REQUIRE((gather_m == nullptr) == (y_gathered == nullptr));
+  SGCN_REQUIRE(!(y_stats && y_gathered) && y_gathered != y);
   SGCN_REQUIRE((rscale == nullptr) == (rshift == nullptr) && (r || !rscale));
   hipStream_t st = (hipStream_t)stream;
   const int res = r == nullptr ? 0 : (rscale ? 2 : 1);
   dim3 g(B * C);
   float2* ys = (float2*)y_stats;
-#define SGCN_APPLY(PJ, RS, RL)                                                                    \
-  (ys ? bn_apply_kernel<PJ, RS, RL, true><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale,     \
-                                                                  rshift, y, ys, C, T, V)         \
-      : bn_apply_kernel<PJ, RS, RL, false><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale,    \
-                                                                   rshift, y, ys, C, T, V))
+#define SGCN_APPLY_X(PJ, RS, RL, OX)                                                        \
+  bn_apply_kernel<PJ, RS, RL, OX><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale, rshift, y, \
+                                                          ys, gather_m, y_gathered, C, T, V)
+#define SGCN_APPLY(PJ, RS, RL)                                                               \
+  (ys ? SGCN_APPLY_X(PJ, RS, RL, 1)                                                          \
+      : (y_gathered ? SGCN_APPLY_X(PJ, RS, RL, 2) : SGCN_APPLY_X(PJ, RS, RL, 0)))
 #define SGCN_APPLY_R(PJ, RL) \
   if (res == 0) SGCN_APPLY(PJ, 0, RL); else if (res == 1) SGCN_APPLY(PJ, 1, RL); else SGCN_APPLY(PJ, 2, RL)
   if (per_joint) { if (relu) { SGCN_APPLY_R(true, true); } else { SGCN_APPLY_R(true, false); } }
   else { if (relu) { SGCN_APPLY_R(false, true); } else { SGCN_APPLY_R(false, false); } }
 #undef SGCN_APPLY_R
 #undef SGCN_APPLY
+#undef SGCN_APPLY_X
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -640,6 +705,7 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
   SGCN_REQUIRE(dy && x && coef && dx && (y || !relu));
   SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE(!rcoef || (r && dr));
+  SGCN_REQUIRE(per_joint >= 0 && per_joint <= 2);
   hipStream_t st = (hipStream_t)stream;
   const int res = dr == nullptr ? 0 : (rcoef ? 2 : 1);
   const int F = per_joint ? C * V : C;
@@ -651,8 +717,9 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                  dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V))
 #define SGCN_BA_R(PJ, RL) \
   if (res == 0) SGCN_BA(PJ, RL, 0); else if (res == 1) SGCN_BA(PJ, RL, 1); else SGCN_BA(PJ, RL, 2)
-  if (per_joint) { if (relu) { SGCN_BA_R(true, true); } else { SGCN_BA_R(true, false); } }
-  else { if (relu) { SGCN_BA_R(false, true); } else { SGCN_BA_R(false, false); } }
+  if (per_joint == 2) { if (relu) { SGCN_BA_R(2, true); } else { SGCN_BA_R(2, false); } }
+  else if (per_joint) { if (relu) { SGCN_BA_R(1, true); } else { SGCN_BA_R(1, false); } }
+  else { if (relu) { SGCN_BA_R(0, true); } else { SGCN_BA_R(0, false); } }
 #undef SGCN_BA_R
 #undef SGCN_BA
   SGCN_LAUNCH_CHECK();
@@ -662,6 +729,16 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
 int sgcn_mask_prep(const float* mask, float* m, int n, void* stream) {
   SGCN_REQUIRE(mask && m && n > 0);
   mask_prep_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(mask, m, n);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, int T, int V,
+                    void* stream) {
+  SGCN_PLANE_CHECK();
+  if (B == 0 || T == 0) return 0;
+  SGCN_REQUIRE(x0 && m && xg && x0 != xg);
+  gcn_gather_kernel<<<B * C, kThreads, 0, (hipStream_t)stream>>>(x0, m, xg, C, T, V);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen: one HIP runtime per proces
 
 LIB_NAME = "libshiftgcn_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 6
+ABI_VERSION = 7
 EINVAL = -22
 
 _lib = None
@@ -42,13 +42,15 @@ SIGNATURES = {
     "sgcn_bn_finalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P,
                               _P]),
     "sgcn_bn_eval_coef": (_I, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P]),
-    "sgcn_bn_apply": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P]),
+    "sgcn_bn_apply": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I,
+                           _P]),
     "sgcn_bn_bwd_reduce": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I,
                                 _I, _P]),
     "sgcn_bn_bwd_finalize": (_I, [_P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
     "sgcn_bn_bwd_apply": (_I, [_P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I,
                                _P]),
     "sgcn_mask_prep": (_I, [_P, _P, _I, _P]),
+    "sgcn_gcn_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "sgcn_gcn_dx_finish": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "sgcn_mask_grad_finalize": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "sgcn_modalities": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),

@@ -5,11 +5,13 @@ launches (no torch compute ops), with its backward written out explicitly so tha
 fusions survive training:
 
 Shift_gcn (shift_gcn.py:121-142)
-  fwd : mask_prep -> pw_fwd[shift_in gather + mask + einsum + bias + shift_out scatter]
+  fwd : mask_prep -> gcn_gather[shift_in gather * mask, kept for the dW]
+        -> pw_fwd[einsum + bias + shift_out scatter]
         -> moments(per joint) -> bn_finalize -> [down: pw_fwd -> moments -> finalize]
         -> bn_apply(+down/identity, ReLU)
-  bwd : bn_bwd_reduce(ReLU mask, both BNs) -> finalize x2 -> bn_bwd_apply
-        -> pw_dw(Linear_weight^T, bias) -> pw_fwd(dX in gathered space)
+  bwd : bn_bwd_reduce(ReLU mask, both BNs) -> finalize x2 -> bn_bwd_apply[dZ stored
+        gathered: shift_out^T in the store] -> pw_dw(Linear_weight^T, bias)
+        -> pw_fwd(dX in gathered space)
         -> gcn_dx_finish(shift_in^T + mask, dmask partials) -> mask_grad_finalize
         -> [down: pw_dw, pw_fwd(accumulate)]
 Shift_tcn (shift_gcn.py:65-74)
@@ -42,16 +44,20 @@ def _empty(*shape, like):
 # Shift_gcn
 # ======================================================================================
 class GcnSaved:
-    __slots__ = ("x0", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
+    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
 
 
 def gcn_forward(mod, x0, training):
     B, Cin, T, V = x0.shape
     Cout = mod.out_channels
-    m = ops.mask_prep(mod.Feature_Mask)
+    cache = mod.__dict__.pop("_gather_cache", None)
+    if cache is not None and cache[0] is x0:
+        xg, m = cache[1], cache[2]    # made by the previous unit's tail from its registers
+    else:
+        m = ops.mask_prep(mod.Feature_Mask)
+        xg = ops.gcn_gather(x0, m)    # shift_in gather * mask, once (reused by the dW)
     Z = _empty(B, Cout, T, V, like=x0)
-    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(x0, 1, +1), PV(Z, 1, +1),
-               Cout, Cin, T, V, mask=m)
+    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z, 1, +1), Cout, Cin, T, V)
     if training:
         zst = ops.bn_finalize(ops.moments(Z, True), B, Cout * V, T, mod.bn, perm_V=V)
     else:
@@ -69,7 +75,7 @@ def gcn_forward(mod, x0, training):
     else:
         H, hm = ops.bn_apply(Z, zst, True, r=x0, relu=True, out_stats=training)
     s = GcnSaved()
-    s.x0, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, Z, zst, D0, dst, H, m
+    s.x0, s.xg, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, xg, Z, zst, D0, dst, H, m
     s.h_moments = hm   # moments of H for Shift_tcn.bn, produced by the same launch
     return H, s
 
@@ -96,19 +102,19 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None):
         coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
             rpart, B, Cout, B * T * V, s.dst, bnd)
         dD0 = _empty(B, Cout, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ,
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ,
                          dy_coef=dy_coef)
     else:
         g_id = _empty(B, Cin, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, True, dr=g_id, dx=dZ, dy_coef=dy_coef)
-    # einsum/bias grads: G(b,d,n) = dZ gathered back through shift_out (rotation +d)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2, dr=g_id, dx=dZ, dy_coef=dy_coef)
+    # dZ is stored gathered (per_joint=2: shift_out transposed by the store), so the
+    # einsum/bias grads and dX read it as a plain plane: G(b,d,n) = dZ[b,d,n]
     dLW = torch.empty_like(mod.Linear_weight)
     dLb = torch.empty_like(mod.Linear_bias)
-    ops.pw_dw(PV(dZ, 1, +1), PV(x0, 1, +1), dLW, Cout, Cin, T, V, mask=s.m, transpose=True,
-              dbias=dLb)
+    ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
     g["Linear_weight"], g["Linear_bias"] = dLW, dLb
     dXt = _empty(B, Cin, T, V, like=x0)
-    ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ, 1, +1), PV(dXt), Cin, Cout, T, V)
+    ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
     dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=extra_dx)
     g["Feature_Mask"] = ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V)
     if mod.has_down:
@@ -235,13 +241,20 @@ def unit_forward(unit, x, training):
     H, gs = gcn_forward(unit.gcn1, x, training)
     S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
     rs = None
+    # the next unit's Shift_gcn (set by Model.forward_planes for the duration of a call):
+    # its gathered, masked input is written by this tail launch too
+    consumer = unit.__dict__.get("_gather_consumer")
+    gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
     if unit.residual_kind == "conv":
         Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
-        out = ops.bn_apply(S, sst, False, r=Rc, rst=rst, relu=True)
+        out = ops.bn_apply(S, sst, False, r=Rc, rst=rst, relu=True, gather_m=gm)
     elif unit.residual_kind == "identity":
-        out = ops.bn_apply(S, sst, False, r=x, relu=True)
+        out = ops.bn_apply(S, sst, False, r=x, relu=True, gather_m=gm)
     else:
-        out = ops.bn_apply(S, sst, False, relu=True)
+        out = ops.bn_apply(S, sst, False, relu=True, gather_m=gm)
+    if gm is not None:
+        out, xg_next = out
+        consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
     s = UnitSaved()
     s.x, s.gs, s.ts, s.rs, s.out = x, gs, ts, rs, out
     return out, s

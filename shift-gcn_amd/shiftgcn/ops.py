@@ -262,19 +262,23 @@ def bn_eval_coef(bn, F, perm_V=0, device=None):
 
 
 def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False, out=None,
-             out_stats=None):
-    """Returns y; with ``out_stats`` given (True/False) returns (y, moments of y or None)."""
+             out_stats=None, gather_m=None):
+    """Returns y; with ``out_stats`` given (True/False) returns (y, moments of y or None);
+    with ``gather_m`` returns (y, gcn_gather(y, gather_m)) from one launch."""
     check_input(x, "input")
     if r is not None:
         check_input(r, "residual")
     B, C, T, V = x.shape
     y = torch.empty_like(x) if out is None else out
     ys = torch.empty((B * C * 2,), device=x.device, dtype=_F32) if out_stats else None
+    yg = torch.empty_like(y) if gather_m is not None else None
     rc = _lib.load().sgcn_bn_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift), int(per_joint),
                                    _ptr(r), _ptr(rst.scale) if rst else None,
                                    _ptr(rst.shift) if rst else None, int(relu), _ptr(y),
-                                   _ptr(ys), B, C, T, V, _stream(x))
+                                   _ptr(ys), _ptr(gather_m), _ptr(yg), B, C, T, V, _stream(x))
     _lib.check(rc, "sgcn_bn_apply")
+    if gather_m is not None:
+        return y, yg
     return y if out_stats is None else (y, ys)
 
 
@@ -325,6 +329,14 @@ def mask_prep(mask):
     rc = _lib.load().sgcn_mask_prep(_ptr(mask), _ptr(m), mask.numel(), _stream(mask))
     _lib.check(rc, "sgcn_mask_prep")
     return m
+
+
+def gcn_gather(x0, m):
+    B, C, T, V = x0.shape
+    xg = torch.empty_like(x0)
+    rc = _lib.load().sgcn_gcn_gather(_ptr(x0), _ptr(m), _ptr(xg), B, C, T, V, _stream(x0))
+    _lib.check(rc, "sgcn_gcn_gather")
+    return xg
 
 
 def gcn_dx_finish(dxt, x0, m, add1=None, add2=None):

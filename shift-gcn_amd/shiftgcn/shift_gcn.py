@@ -199,8 +199,17 @@ class Model(nn.Module):
     def forward_planes(self, x, N, M):
         """Body + head of ``forward`` (shift_gcn.py:200-216) on an input already permuted
         to (N*M, C, T, V) and normalised by ``data_bn`` (e.g. by ``sgcn_modalities``)."""
-        for k in range(1, 11):
-            x = getattr(self, f"l{k}")(x)
+        units = [getattr(self, f"l{k}") for k in range(1, 11)]
+        try:
+            # each unit's tail launch also writes the next unit's gathered gcn input
+            for u, nxt in zip(units[:-1], units[1:]):
+                u.__dict__["_gather_consumer"] = nxt.gcn1
+            for u in units:
+                x = u(x)
+        finally:
+            for u in units:
+                u.__dict__.pop("_gather_consumer", None)
+                u.gcn1.__dict__.pop("_gather_cache", None)
         c_new = x.size(1)
         x = x.view(N, M, c_new, -1)
         x = x.mean(3).mean(1)

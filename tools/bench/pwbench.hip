@@ -70,6 +70,17 @@ void dw_variant(const char* name, const Shape& s, DwArgs a, int S, hipStream_t s
   }
 }
 
+template <int BM, int BN, int WM, int WN>
+void fwd_variant(const Shape& s, const FwdArgs& a, hipStream_t st, const float* yref,
+                 double fl, double by) {
+  if (a.M > BM) return;
+  auto L = [&]() { launch_pwg<BM, BN, WM, WN>(a, false, st); };
+  float us = timeit(L, st, 20);
+  const size_t n = (size_t)s.B * s.M * s.T * s.V;
+  printf("%-20s fwd %3dx%3d w%dx%d            %8.1f us  %6.1f TF/s  %6.2f TB/s  %s\n", s.name,
+         BM, BN, WM, WN, us, fl / us / 1e6, by / us / 1e6, same(yref, a.y.ptr, n) ? "bit-exact" : "MISMATCH");
+}
+
 int main(int argc, char** argv) {
   const bool do_fwd = argc < 2 || strchr(argv[1], 'f');
   const bool do_dw = argc < 2 || strchr(argv[1], 'w');
@@ -112,6 +123,26 @@ int main(int argc, char** argv) {
       float us = timeit(L, st, 20);
       printf("%-20s %-26s %8.1f us  %6.1f TF/s  %6.2f TB/s\n", s.name, "fwd product", us,
              fl / us / 1e6, by / us / 1e6);
+      if (argc > 2) {
+        FwdArgs v = a;
+        v.y.ptr = y3;
+        v.x_bytes = plane_bytes(v.x.bstride, v.x.cstride, 1, s.B, s.K, s.T, s.V);
+        v.y_bytes = plane_bytes(v.y.bstride, v.y.cstride, 1, s.B, s.M, s.T, s.V);
+        v.a_bytes = (unsigned)(s.M * s.K * 4);
+        v.mask_bytes = s.mask ? (unsigned)(s.V * s.K * 4) : 0u;
+        fwd_variant<64, 256, 2, 4>(s, v, st, y2, fl, by);
+        fwd_variant<64, 128, 1, 4>(s, v, st, y2, fl, by);
+        fwd_variant<64, 512, 2, 4>(s, v, st, y2, fl, by);
+        fwd_variant<64, 256, 1, 4>(s, v, st, y2, fl, by);
+        fwd_variant<128, 256, 2, 4>(s, v, st, y2, fl, by);
+        fwd_variant<128, 128, 2, 2>(s, v, st, y2, fl, by);
+        fwd_variant<128, 128, 4, 2>(s, v, st, y2, fl, by);
+        fwd_variant<256, 128, 4, 2>(s, v, st, y2, fl, by);
+        fwd_variant<256, 64, 4, 1>(s, v, st, y2, fl, by);
+        fwd_variant<256, 128, 4, 1>(s, v, st, y2, fl, by);
+        fwd_variant<256, 256, 4, 2>(s, v, st, y2, fl, by);
+        fwd_variant<256, 64, 4, 2>(s, v, st, y2, fl, by);
+      }
     }
     if (do_dw) {
       // dW[m][c] = sum_p G(m,p) X(c,p): G = y (M rows), X = x (K rows)
