@@ -398,21 +398,43 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
     float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
     int Hb, int W, int Ho, int add_half) {
-  extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input]
+  // STRIDE == 1 ("re-associated"): only gout is staged (half the LDS -> twice the
+  // workgroups per CU); each thread's own input elements are loaded into registers with
+  // the staging loads, and the position-gradient sums are accumulated over INPUT positions
+  // in pass (1) from the same gout neighbourhood:
+  //   sum_o g[o] * dq(o)/dy = sum_i in[i] * sum_k w'_k g[i - off_k]
+  // (exact adjoint identity; only the summation order differs from the reference's
+  // sum over outputs, and the constraint keeps only the sign of the sum, .cu:370-395).
+  constexpr bool RA = STRIDE == 1;
+  extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input (STRIDE 2 only)]
   __shared__ float red[2 * NT / 64];
   const int plane = blockIdx.x;
   const int c = plane % C;
   const int nb = Hb * W, nt = Ho * W;
   float* gs = lds;
   float* xs = lds + nt;
+  float rin_r[RA ? LPT : 1];
   float bmu = 0.f, bis = 0.f;
   if (BNP) { bmu = bn_mean[c]; bis = bn_invstd[c]; }
   const float x = xpos[c];
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
-  // one staging pass: both planes' loads in flight together (LPT covers nt + nb)
-  {
+  if (RA) {   // gout -> LDS, own input elements -> registers, all loads in flight together
+    const float* __restrict__ go = gout + (size_t)plane * nt;
+    const float* __restrict__ src = in + (size_t)plane * nb;
+    float t[LPT];
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      t[e] = go[min(e * NT + (int)threadIdx.x, nt - 1)];
+      rin_r[e] = src[min(e * NT + (int)threadIdx.x, nb - 1)];
+    }
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int i = e * NT + threadIdx.x;
+      if (i < nt) lds[i] = t[e];
+    }
+  } else {  // one staging pass: both planes' loads in flight together (LPT covers nt + nb)
     const float* __restrict__ go = gout + (size_t)plane * nt;
     const float* __restrict__ src = in + (size_t)plane * nb;
     const int ntot = nt + nb;
@@ -433,7 +455,41 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
 
   // (1) grad_input over the bottom grid (.cu:108-150 stride 1; .cu:191-254 stride 2)
   float bs0 = 0.f, bs1 = 0.f;
-  {
+  float ax = 0.f, ay = 0.f;
+  if (RA) {
+    const Geom r = make_geom(-x, -y);
+    const Geom g = make_geom(x, y);
+    Walker pos(threadIdx.x, NT, W);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int o = e * NT + threadIdx.x;
+      if (o < nb) {
+        TapIdx ti;
+        tap_idx(pos.h + r.y1, pos.w + r.x1, Ho, W, ti);
+        const float q11 = sel(gs[ti.o00], ti.m00), q21 = sel(gs[ti.o01], ti.m01);
+        const float q12 = sel(gs[ti.o10], ti.m10), q22 = sel(gs[ti.o11], ti.m11);
+        float val = blend(q11, q21, q12, q22, r.dx, r.dy);
+        const float rin = rin_r[e];
+        if (RELU_MASK) val = rin > 0.f ? val : 0.f;
+        gi[o] = val;
+        if (BNP) {
+          bs0 += val;
+          bs1 += val * ((rin - bmu) * bis);
+        }
+        // gout at i - off_k for the forward taps off_k = (y1 + a, x1 + b)
+        TapIdx tj;
+        tap_idx(pos.h - g.y1 - 1, pos.w - g.x1 - 1, Ho, W, tj);
+        const float G11 = sel(gs[tj.o11], tj.m11), G21 = sel(gs[tj.o10], tj.m10);
+        const float G12 = sel(gs[tj.o01], tj.m01), G22 = sel(gs[tj.o00], tj.m00);
+        const float cx = (1.f - g.dy) * (G21 - G11) + g.dy * (G22 - G12);
+        const float cy = (1.f - g.dx) * (G12 - G11) + g.dx * (G22 - G21);
+        const float qa = AFFINE ? rin * a + b : rin;
+        ax += qa * cx;
+        ay += qa * cy;
+      }
+      pos.next();
+    }
+  } else {
     const Geom r = make_geom(-x, -y);
     Walker pos(threadIdx.x, NT, W);
     for (int o = threadIdx.x; o < nb; o += NT) {
@@ -470,8 +526,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   }
 
   // (2) position gradients over the top grid (.cu:321-349), summed over the plane
-  float ax = 0.f, ay = 0.f;
-  {
+  if (!RA) {
     const Geom g = make_geom(x, y);
     Walker pos(threadIdx.x, NT, W);
     for (int o = threadIdx.x; o < nt; o += NT) {
@@ -607,7 +662,7 @@ void launch_bwd_lds(bool affine, bool relu, const float* gout, const float* in,
                     float2* pg, float2* bp, int B, int C, int H, int W, int Ho, int add_half,
                     hipStream_t st) {
   dim3 grid(B * C), block(kBwdThreads);
-  const size_t lds = (size_t)(H + Ho) * W * sizeof(float);
+  const size_t lds = (size_t)(STRIDE == 1 ? Ho : H + Ho) * W * sizeof(float);
 #define SGCN_BWDL(A, R, P)                                                                  \
   tshift_bwd_lds_kernel<kBwdThreads, LPT, A, R, STRIDE, P><<<grid, block, lds, st>>>(      \
       gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, Ho, add_half)
@@ -696,7 +751,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   float2* bp = (float2*)bn_part;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
   if ((H + Ho) * W <= kBwdLdsMax && H > 0) {
-    const int lpt = pick_lpt((H + Ho) * W, kBwdThreads);
+    const int lpt = pick_lpt(stride == 1 ? H * W : (H + Ho) * W, kBwdThreads);
 #define SGCN_BWDL_LPT(L)                                                                      \
   (stride == 1 ? launch_bwd_lds<L, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,  \
                                       bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st) \
