@@ -314,7 +314,8 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
 // Same expressions in the same order as the global-tap kernels above, so the results
 // are bit-identical to them (and to the oracle).
 // ------------------------------------------------------------------------------------
-constexpr int kFwdLdsMax = 8192;    // floats of the staged input plane (32 KiB)
+constexpr int kFwdLdsMax = 8192;    // floats of the staged input plane (32 KiB), 256 threads
+constexpr int kFwdLdsMax2 = 16384;  // ... with 512 threads (e.g. MediaPipe T=300: 9,900)
 constexpr int kBwdLdsMax = 16384;   // floats of the staged gout + input planes (64 KiB)
 
 // copy n floats src -> lds (optionally x*a+b), all loads of a thread issued before any
@@ -610,15 +611,15 @@ void launch_fwd(bool affine, bool stats, const float* in, float* out, const floa
 }
 
 // LDS path: EPT = LPT (the output plane is never larger than the staged input plane)
-template <int LPT>
+template <int LPT, int NT = kThreads>
 void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const float* xpos,
                     const float* ypos, const float* scale, const float* shift, float2* ps,
                     int B, int C, int H, int W, int Ho, int stride, int add_half,
                     hipStream_t st) {
-  dim3 grid(B * C), block(kThreads);
+  dim3 grid(B * C), block(NT);
   const size_t lds = (size_t)H * W * sizeof(float);
 #define SGCN_FWDL(A, S)                                                                  \
-  tshift_fwd_lds_kernel<kThreads, LPT, LPT, A, S><<<grid, block, lds, st>>>(            \
+  tshift_fwd_lds_kernel<NT, LPT, LPT, A, S><<<grid, block, lds, st>>>(                  \
       in, out, xpos, ypos, scale, shift, ps, C, H, W, Ho, stride, add_half)
   if (affine) {
     if (stats) SGCN_FWDL(true, true); else SGCN_FWDL(true, false);
@@ -721,6 +722,11 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
     SGCN_LAUNCH_CHECK();
     return 0;
   }
+  if (H * W <= kFwdLdsMax2) {   // 512 threads x 32 staged elements
+    launch_fwd_lds<32, 512>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st);
+    SGCN_LAUNCH_CHECK();
+    return 0;
+  }
   switch (pick_ept(Ho * W)) {
     case 8: launch_fwd<8>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
     case 16: launch_fwd<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
@@ -750,7 +756,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   float2* pg = (float2*)ws;
   float2* bp = (float2*)bn_part;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
-  if ((H + Ho) * W <= kBwdLdsMax && H > 0) {
+  if ((stride == 1 ? H : H + Ho) * W <= kBwdLdsMax && H > 0) {
     const int lpt = pick_lpt(stride == 1 ? H * W : (H + Ho) * W, kBwdThreads);
 #define SGCN_BWDL_LPT(L)                                                                      \
   (stride == 1 ? launch_bwd_lds<L, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,  \

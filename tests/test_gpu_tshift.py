@@ -42,6 +42,9 @@ def test_shift_matches_golden_bit_exact(golden, case):
 @pytest.mark.parametrize("stride", [1, 2])
 @pytest.mark.parametrize("shape", [(2, 64, 300, 25), (3, 16, 75, 33), (1, 5, 1, 25),
                                    (2, 3, 301, 25), (2, 4, 150, 25),
+                                   # MediaPipe planes (300*33 = 9,900 floats) and larger:
+                                   # the 512-thread LDS kernels
+                                   (2, 8, 300, 33), (1, 4, 600, 25),
                                    # planes too large for the LDS-staged kernels: the
                                    # global-tap kernels must agree bit for bit too
                                    (1, 4, 700, 25)])
