@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 7
+#define SGCN_ABI_VERSION 8
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -48,6 +48,19 @@ int sgcn_abi_version(void);
 int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float* ypos,
                     const float* in_scale, const float* in_shift, float* plane_stats,
                     int B, int C, int H, int W, int stride, int ypos_is_raw, void* stream);
+
+/* Inference-mode unit tail fused into Shift_tcn's shift_out forward (shift_gcn.py:72-73,
+ * 161-162, BatchNorms in eval mode): out = relu(shift(in)*post_scale[c] + post_shift[c]
+ * + res), res = 0 (r NULL), r (identity residual) or r*r_scale[c] + r_shift[c] (residual
+ * tcn conv output with its eval BN), r laid out like out. gather_m/out_gathered (both or
+ * neither): also out_gathered = sgcn_gcn_gather(out, gather_m) for the next unit. The
+ * shifted tensor itself is never written. Planes with H*W <= 16384 only (else
+ * SGCN_EINVAL: use sgcn_tshift_fwd + sgcn_bn_apply). */
+int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const float* ypos,
+                         const float* post_scale, const float* post_shift, const float* r,
+                         const float* r_scale, const float* r_shift, const float* gather_m,
+                         float* out_gathered, int B, int C, int H, int W, int stride,
+                         int ypos_is_raw, void* stream);
 
 /* Workspace bytes for sgcn_tshift_bwd (B*C float2 plane partials). */
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C);

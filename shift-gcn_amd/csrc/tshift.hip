@@ -391,6 +391,66 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
   if (STATS && threadIdx.x == 0) pstats[plane] = make_float2((float)run_mean, (float)run_m2);
 }
 
+// Inference unit tail fused into the shift_out forward (shift_gcn.py:72-73 + 161-162 with
+// the BatchNorms in eval mode): out = relu(S*ps[c] + pt[c] + res), S the shifted value,
+// res = 0 (RES 0), r (RES 1, identity residual) or r*rs[c] + rt[c] (RES 2, residual tcn
+// conv output + eval BN), read at the output address; GOUT: also the next Shift_gcn's
+// gathered, masked input og[c,t,(v - c) mod V] = out[c,t,v] * gm[((v - c) mod V)*C + c].
+// S is never written. Same tap arithmetic as tshift_fwd_lds_kernel.
+template <int NT, int LPT, int RES, bool GOUT>
+__global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
+    const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
+    const float* __restrict__ ypos, const float* __restrict__ ps, const float* __restrict__ pt,
+    const float* __restrict__ r, const float* __restrict__ rs, const float* __restrict__ rt,
+    const float* __restrict__ gm, float* __restrict__ og, int C, int Hb, int W, int Ho,
+    int stride, int add_half) {
+  extern __shared__ float pl[];   // Hb*W staged input
+  __shared__ float gm_s[GOUT ? 1024 : 1];
+  const int plane = blockIdx.x;
+  const int c = plane % C;
+  const size_t ooff = (size_t)plane * Ho * W;
+  const float y = add_half ? ypos[c] + 0.5f : ypos[c];
+  const Geom g = make_geom(xpos[c], y);
+  const float sc = ps[c], sh = pt[c];
+  float q1 = 1.f, q2 = 0.f;
+  if (RES == 2) { q1 = rs[c]; q2 = rt[c]; }
+  const int rc = c % W;
+  if (GOUT)
+    for (int i = threadIdx.x; i < W; i += NT) gm_s[i] = gm[i * C + c];
+  stage_plane<NT, LPT, false>(in + (size_t)plane * Hb * W, pl, Hb * W, 1.f, 0.f);
+  __syncthreads();
+  const int n = Ho * W;
+  for (int base = 0; base < n; base += LPT * NT) {
+    Walker pos(base + threadIdx.x, NT, W);
+    float rv[LPT];
+    if (RES) {
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) rv[e] = r[ooff + min(base + e * NT + (int)threadIdx.x, n - 1)];
+    }
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      TapIdx ti;
+      tap_idx(pos.h * stride + g.y1, pos.w + g.x1, Hb, W, ti);
+      const float q11 = sel(pl[ti.o00], ti.m00), q21 = sel(pl[ti.o01], ti.m01);
+      const float q12 = sel(pl[ti.o10], ti.m10), q22 = sel(pl[ti.o11], ti.m11);
+      const int o = base + e * NT + threadIdx.x;
+      float a = blend(q11, q21, q12, q22, g.dx, g.dy) * sc + sh;
+      if (RES == 1) a += rv[e];
+      if (RES == 2) a += rv[e] * q1 + q2;
+      a = fmaxf(a, 0.f);
+      if (o < n) {
+        out[ooff + o] = a;
+        if (GOUT) {
+          int u = pos.w - rc;
+          u = u < 0 ? u + W : u;
+          og[ooff + o - pos.w + u] = a * gm_s[u];
+        }
+      }
+      pos.next();
+    }
+  }
+}
+
 template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP>
 __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
@@ -732,6 +792,49 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
     case 16: launch_fwd<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
     default: launch_fwd<32>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
   }
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const float* ypos,
+                         const float* post_scale, const float* post_shift, const float* r,
+                         const float* r_scale, const float* r_shift, const float* gather_m,
+                         float* out_gathered, int B, int C, int H, int W, int stride,
+                         int ypos_is_raw, void* stream) {
+  SGCN_REQUIRE(B >= 0 && C > 0 && H >= 0 && W > 0 && W <= 1024 && stride >= 1);
+  SGCN_REQUIRE((r_scale == nullptr) == (r_shift == nullptr) && (r || !r_scale));
+  SGCN_REQUIRE((gather_m == nullptr) == (out_gathered == nullptr));
+  SGCN_REQUIRE(H * W <= kFwdLdsMax2);   // LDS-staged planes only (caller falls back)
+  const int Ho = H / stride;
+  if (B == 0 || Ho == 0) return 0;
+  SGCN_REQUIRE(in && out && xpos && ypos && post_scale && post_shift && out != in);
+  SGCN_REQUIRE((long long)B * C < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
+  const int res = r == nullptr ? 0 : (r_scale ? 2 : 1);
+  const bool go = out_gathered != nullptr;
+  const size_t lds = (size_t)H * W * sizeof(float);
+#define SGCN_TAIL(NT, L, R, G)                                                                \
+  tshift_fwd_tail_kernel<NT, L, R, G><<<B * C, NT, lds, st>>>(                                \
+      in, out, xpos, ypos, post_scale, post_shift, r, r_scale, r_shift, gather_m,            \
+      out_gathered, C, H, W, Ho, stride, ah)
+#define SGCN_TAIL_RG(NT, L)                                                                   \
+  do {                                                                                        \
+    if (res == 0) { if (go) SGCN_TAIL(NT, L, 0, true); else SGCN_TAIL(NT, L, 0, false); }     \
+    else if (res == 1) { if (go) SGCN_TAIL(NT, L, 1, true); else SGCN_TAIL(NT, L, 1, false); } \
+    else { if (go) SGCN_TAIL(NT, L, 2, true); else SGCN_TAIL(NT, L, 2, false); }              \
+  } while (0)
+  if (H * W <= kFwdLdsMax) {
+    switch (pick_lpt(H * W, kThreads)) {
+      case 8: SGCN_TAIL_RG(kThreads, 8); break;
+      case 16: SGCN_TAIL_RG(kThreads, 16); break;
+      default: SGCN_TAIL_RG(kThreads, 32); break;
+    }
+  } else {
+    SGCN_TAIL_RG(512, 32);
+  }
+#undef SGCN_TAIL_RG
+#undef SGCN_TAIL
   SGCN_LAUNCH_CHECK();
   return 0;
 }

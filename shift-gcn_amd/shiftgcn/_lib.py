@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen: one HIP runtime per proces
 
 LIB_NAME = "libshiftgcn_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 7
+ABI_VERSION = 8
 EINVAL = -22
 
 _lib = None
@@ -29,6 +29,8 @@ _L = ctypes.c_longlong
 SIGNATURES = {
     "sgcn_abi_version": (_I, []),
     "sgcn_tshift_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "sgcn_tshift_fwd_tail": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
+                                  _I, _I, _P]),
     "sgcn_tshift_bwd_ws_bytes": (_Z, [_I, _I]),
     "sgcn_tshift_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _Z, _I,
                              _I, _I, _I, _I, _I, _P]),

@@ -30,6 +30,8 @@ caching allocator, so a whole training step can be captured in a hipGraph.
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 
 from . import ops
@@ -133,7 +135,7 @@ class TcnSaved:
     __slots__ = ("H", "ast", "As", "R", "S", "sst")
 
 
-def tcn_core_forward(mod, H, training, h_moments=None):
+def tcn_core_forward(mod, H, training, h_moments=None, tail=None):
     """bn -> shift_in -> temporal_linear -> ReLU -> shift_out; returns (S, bn2 stats, saved)
     where S is the shift_out output BEFORE bn2. ``h_moments``: per-plane moments of H
     already produced by the launch that wrote H (else computed here)."""
@@ -153,6 +155,11 @@ def tcn_core_forward(mod, H, training, h_moments=None):
     tl = mod.temporal_linear
     ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
     To = T // stride
+    if tail is not None:
+        # inference: bn2 (eval) + residual + ReLU (+ next gather) fused into shift_out
+        sst = ops.bn_eval_coef(mod.bn2, Cout)
+        return ops.tshift_fwd_tail(R, so.xpos.detach(), so.ypos.detach(), stride, sst,
+                                   r=tail[0], rst=tail[1], gather_m=tail[2])
     stats = _empty(B * Cout * 2, like=H) if training else None
     S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
     if training:
@@ -238,12 +245,26 @@ class UnitSaved:
 
 
 def unit_forward(unit, x, training):
+    consumer = unit.__dict__.get("_gather_consumer")
+    if (not training and _INFER.active and
+            x.shape[2] * x.shape[3] <= ops.TAIL_MAX_PLANE):
+        # inference (no backward can follow): the unit tail is fused into shift_out
+        H, gs = gcn_forward(unit.gcn1, x, training)
+        r = rst = None
+        if unit.residual_kind == "conv":
+            r, rst, _ = convbn_core_forward(unit.residual, x, training)
+        elif unit.residual_kind == "identity":
+            r = x
+        gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
+        out, xg_next = tcn_core_forward(unit.tcn1, H, training, tail=(r, rst, gm))
+        if gm is not None:
+            consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
+        return out, None
     H, gs = gcn_forward(unit.gcn1, x, training)
     S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
     rs = None
     # the next unit's Shift_gcn (set by Model.forward_planes for the duration of a call):
     # its gathered, masked input is written by this tail launch too
-    consumer = unit.__dict__.get("_gather_consumer")
     gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
     if unit.residual_kind == "conv":
         Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
@@ -327,9 +348,25 @@ class _BlockFunction(torch.autograd.Function):
         return (None, None, dx) + tuple(grads.get(n) for n in ctx.names)
 
 
+class _InferFlag(threading.local):
+    active = False
+
+
+# set while a block runs with no backward possible (grad disabled, or nothing requires
+# grad; autograd Functions always run forward with grad disabled, so it is decided here):
+# eval-mode blocks may then skip tensors only a backward would read
+_INFER = _InferFlag()
+
+
 def run_block(impl, module, x):
     params = [p for _, p in trainable(module)]
-    return _BlockFunction.apply(impl, module, x, *params)
+    prev = _INFER.active
+    _INFER.active = not (torch.is_grad_enabled() and
+                         (x.requires_grad or any(p.requires_grad for p in params)))
+    try:
+        return _BlockFunction.apply(impl, module, x, *params)
+    finally:
+        _INFER.active = prev
 
 
 def _gcn_standalone_bwd(mod, s, dy):

@@ -124,6 +124,28 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
     return out
 
 
+TAIL_MAX_PLANE = 16384   # sgcn_tshift_fwd_tail: LDS-staged planes only
+
+
+def tshift_fwd_tail(inp, xpos, ypos, stride, st, r=None, rst=None, gather_m=None):
+    """Inference unit tail: relu(BN_eval(shift(inp)) + res) in one launch (+ the next
+    unit's gathered gcn input when ``gather_m`` is given). Returns (out, gathered|None)."""
+    check_input(inp, "input")
+    if r is not None:
+        check_input(r, "residual")
+    B, C, H, W = inp.shape
+    out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
+    og = torch.empty_like(out) if gather_m is not None else None
+    nb = 4 * (inp.numel() + out.numel() * (1 + (r is not None) + (og is not None)))
+    with _timed("tshift_fwd", 0, nb, inp):
+        rc = _lib.load().sgcn_tshift_fwd_tail(
+            _ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(st.scale), _ptr(st.shift),
+            _ptr(r), _ptr(rst.scale) if rst else None, _ptr(rst.shift) if rst else None,
+            _ptr(gather_m), _ptr(og), B, C, H, W, stride, 1, _stream(inp))
+    _lib.check(rc, "sgcn_tshift_fwd_tail")
+    return out, og
+
+
 def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=False,
                ypos_is_raw=True, bn_stats=None):
     """Backward shift: returns (grad_input, grad_xpos, grad_ypos), plus the BatchNorm
