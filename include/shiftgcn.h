@@ -49,6 +49,17 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
                     const float* in_scale, const float* in_shift, float* plane_stats,
                     int B, int C, int H, int W, int stride, int ypos_is_raw, void* stream);
 
+/* Inference-mode Shift_gcn tail fused into Shift_tcn's shift_in forward (shift_gcn.py:
+ * 137-141 then 67-68, BatchNorms in eval mode): out = shift(in_scale[c]*H + in_shift[c]),
+ * H = relu(z*pre_scale[c*W+w] + pre_shift[c*W+w] + res) formed while staging, z the gcn
+ * contraction output Z, res = r (identity down) or r*r_scale[c] + r_shift[c] (down conv
+ * output with its eval BN). H is never written. H*W <= 16384 only (else SGCN_EINVAL). */
+int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const float* ypos,
+                        const float* pre_scale, const float* pre_shift, const float* r,
+                        const float* r_scale, const float* r_shift, const float* in_scale,
+                        const float* in_shift, int B, int C, int H, int W, int stride,
+                        int ypos_is_raw, void* stream);
+
 /* Inference-mode unit tail fused into Shift_tcn's shift_out forward (shift_gcn.py:72-73,
  * 161-162, BatchNorms in eval mode): out = relu(shift(in)*post_scale[c] + post_shift[c]
  * + res), res = 0 (r NULL), r (identity residual) or r*r_scale[c] + r_shift[c] (residual

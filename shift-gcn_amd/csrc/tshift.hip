@@ -391,6 +391,72 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
   if (STATS && threadIdx.x == 0) pstats[plane] = make_float2((float)run_mean, (float)run_m2);
 }
 
+// Inference Shift_gcn tail fused into the following shift_in forward (shift_gcn.py:137-141
+// then :67-68, BatchNorms in eval mode): the staged input element is
+//   a * relu(z*zs[c*W + w] + zt[c*W + w] + res) + b
+// with z the contraction output Z (natural layout), res = r (identity down) or
+// r*rs[c] + rt[c] (down conv output + eval BN), a/b = Shift_tcn.bn (eval); the gcn
+// output H is never written. Same tap arithmetic as tshift_fwd_lds_kernel.
+template <int NT, int LPT, int RES>
+__global__ __launch_bounds__(NT) void tshift_fwd_pre_kernel(
+    const float* __restrict__ z, float* __restrict__ out, const float* __restrict__ xpos,
+    const float* __restrict__ ypos, const float* __restrict__ zs, const float* __restrict__ zt,
+    const float* __restrict__ r, const float* __restrict__ rs, const float* __restrict__ rt,
+    const float* __restrict__ scale, const float* __restrict__ shift, int C, int Hb, int W,
+    int Ho, int stride, int add_half) {
+  extern __shared__ float pl[];   // Hb*W staged input
+  __shared__ float zs_s[1024], zt_s[1024];
+  const int plane = blockIdx.x;
+  const int c = plane % C;
+  const int nb = Hb * W;
+  const size_t ioff = (size_t)plane * nb;
+  float* __restrict__ dst = out + (size_t)plane * Ho * W;
+  const float y = add_half ? ypos[c] + 0.5f : ypos[c];
+  const Geom g = make_geom(xpos[c], y);
+  const float a = scale[c], b = shift[c];
+  float q1 = 1.f, q2 = 0.f;
+  if (RES == 2) { q1 = rs[c]; q2 = rt[c]; }
+  for (int i = threadIdx.x; i < W; i += NT) {
+    zs_s[i] = zs[c * W + i];
+    zt_s[i] = zt[c * W + i];
+  }
+  __syncthreads();
+  {
+    float t[LPT], u[LPT];
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int i = min(e * NT + (int)threadIdx.x, nb - 1);
+      t[e] = z[ioff + i];
+      u[e] = r[ioff + i];
+    }
+    Walker pos(threadIdx.x, NT, W);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int i = e * NT + threadIdx.x;
+      float h = t[e] * zs_s[pos.w] + zt_s[pos.w];
+      h += RES == 2 ? u[e] * q1 + q2 : u[e];
+      h = fmaxf(h, 0.f);
+      if (i < nb) pl[i] = h * a + b;
+      pos.next();
+    }
+  }
+  __syncthreads();
+  const int n = Ho * W;
+  for (int base = 0; base < n; base += LPT * NT) {
+    Walker pos(base + threadIdx.x, NT, W);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      TapIdx ti;
+      tap_idx(pos.h * stride + g.y1, pos.w + g.x1, Hb, W, ti);
+      const float q11 = sel(pl[ti.o00], ti.m00), q21 = sel(pl[ti.o01], ti.m01);
+      const float q12 = sel(pl[ti.o10], ti.m10), q22 = sel(pl[ti.o11], ti.m11);
+      const int o = base + e * NT + threadIdx.x;
+      if (o < n) dst[o] = blend(q11, q21, q12, q22, g.dx, g.dy);
+      pos.next();
+    }
+  }
+}
+
 // Inference unit tail fused into the shift_out forward (shift_gcn.py:72-73 + 161-162 with
 // the BatchNorms in eval mode): out = relu(S*ps[c] + pt[c] + res), S the shifted value,
 // res = 0 (RES 0), r (RES 1, identity residual) or r*rs[c] + rt[c] (RES 2, residual tcn
@@ -792,6 +858,44 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
     case 16: launch_fwd<16>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
     default: launch_fwd<32>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;
   }
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const float* ypos,
+                        const float* pre_scale, const float* pre_shift, const float* r,
+                        const float* r_scale, const float* r_shift, const float* in_scale,
+                        const float* in_shift, int B, int C, int H, int W, int stride,
+                        int ypos_is_raw, void* stream) {
+  SGCN_REQUIRE(B >= 0 && C > 0 && H >= 0 && W > 0 && W <= 1024 && stride >= 1);
+  SGCN_REQUIRE((r_scale == nullptr) == (r_shift == nullptr));
+  SGCN_REQUIRE(H * W <= kFwdLdsMax2);   // LDS-staged planes only (caller falls back)
+  const int Ho = H / stride;
+  if (B == 0 || Ho == 0) return 0;
+  SGCN_REQUIRE(z && out && xpos && ypos && pre_scale && pre_shift && r && in_scale &&
+               in_shift && out != z);
+  SGCN_REQUIRE((long long)B * C < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
+  const size_t lds = (size_t)H * W * sizeof(float);
+#define SGCN_PRE(NT, L, R)                                                                     \
+  tshift_fwd_pre_kernel<NT, L, R><<<B * C, NT, lds, st>>>(z, out, xpos, ypos, pre_scale,       \
+                                                           pre_shift, r, r_scale, r_shift,     \
+                                                           in_scale, in_shift, C, H, W, Ho,    \
+                                                           stride, ah)
+#define SGCN_PRE_R(NT, L) \
+  do { if (r_scale) SGCN_PRE(NT, L, 2); else SGCN_PRE(NT, L, 1); } while (0)
+  if (H * W <= kFwdLdsMax) {
+    switch (pick_lpt(H * W, kThreads)) {
+      case 8: SGCN_PRE_R(kThreads, 8); break;
+      case 16: SGCN_PRE_R(kThreads, 16); break;
+      default: SGCN_PRE_R(kThreads, 32); break;
+    }
+  } else {
+    SGCN_PRE_R(512, 32);
+  }
+#undef SGCN_PRE_R
+#undef SGCN_PRE
   SGCN_LAUNCH_CHECK();
   return 0;
 }

@@ -29,6 +29,8 @@ _L = ctypes.c_longlong
 SIGNATURES = {
     "sgcn_abi_version": (_I, []),
     "sgcn_tshift_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "sgcn_tshift_fwd_pre": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
+                                 _I, _I, _P]),
     "sgcn_tshift_fwd_tail": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
                                   _I, _I, _P]),
     "sgcn_tshift_bwd_ws_bytes": (_Z, [_I, _I]),

@@ -135,11 +135,33 @@ class TcnSaved:
     __slots__ = ("H", "ast", "As", "R", "S", "sst")
 
 
-def tcn_core_forward(mod, H, training, h_moments=None, tail=None):
+def gcn_infer_z(mod, x0):
+    """Inference Shift_gcn up to its contraction output: (Z, zst, res, res_stats); the
+    BN1d + down/identity + ReLU are applied by the consumer (sgcn_tshift_fwd_pre)."""
+    B, Cin, T, V = x0.shape
+    Cout = mod.out_channels
+    cache = mod.__dict__.pop("_gather_cache", None)
+    if cache is not None and cache[0] is x0:
+        xg = cache[1]
+    else:
+        xg = ops.gcn_gather(x0, ops.mask_prep(mod.Feature_Mask))
+    Z = _empty(B, Cout, T, V, like=x0)
+    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z, 1, +1), Cout, Cin, T, V)
+    zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
+    if mod.has_down:
+        conv, bn = mod.down[0], mod.down[1]
+        D0 = _empty(B, Cout, T, V, like=x0)
+        ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
+        return Z, zst, D0, ops.bn_eval_coef(bn, Cout)
+    return Z, zst, x0, None
+
+
+def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
     """bn -> shift_in -> temporal_linear -> ReLU -> shift_out; returns (S, bn2 stats, saved)
     where S is the shift_out output BEFORE bn2. ``h_moments``: per-plane moments of H
     already produced by the launch that wrote H (else computed here)."""
-    B, C, T, V = H.shape
+    src = H if H is not None else pre[0]
+    B, C, T, V = src.shape
     Cout = mod.out_channels
     si, so = mod.shift_in, mod.shift_out
     stride = so.stride
@@ -149,9 +171,13 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None):
         ast = ops.bn_finalize(h_moments, B, C, T * V, mod.bn)
     else:
         ast = ops.bn_eval_coef(mod.bn, C)
-    As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=ast.scale,
-                        shift=ast.shift)
-    R = _empty(B, Cout, T, V, like=H)
+    if pre is not None:   # inference: H = relu(BN1d(Z) + res) formed while staging
+        As = ops.tshift_fwd_pre(pre[0], si.xpos.detach(), si.ypos.detach(), si.stride, pre[1],
+                                pre[2], pre[3], ast)
+    else:
+        As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride,
+                            scale=ast.scale, shift=ast.shift)
+    R = _empty(B, Cout, T, V, like=src)
     tl = mod.temporal_linear
     ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
     To = T // stride
@@ -160,7 +186,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None):
         sst = ops.bn_eval_coef(mod.bn2, Cout)
         return ops.tshift_fwd_tail(R, so.xpos.detach(), so.ypos.detach(), stride, sst,
                                    r=tail[0], rst=tail[1], gather_m=tail[2])
-    stats = _empty(B * Cout * 2, like=H) if training else None
+    stats = _empty(B * Cout * 2, like=src) if training else None
     S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
     if training:
         sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2)
@@ -248,15 +274,17 @@ def unit_forward(unit, x, training):
     consumer = unit.__dict__.get("_gather_consumer")
     if (not training and _INFER.active and
             x.shape[2] * x.shape[3] <= ops.TAIL_MAX_PLANE):
-        # inference (no backward can follow): the unit tail is fused into shift_out
-        H, gs = gcn_forward(unit.gcn1, x, training)
+        # inference (no backward can follow): the Shift_gcn tail is fused into shift_in,
+        # the unit tail into shift_out; neither H nor S is written
+        pre = gcn_infer_z(unit.gcn1, x)
         r = rst = None
         if unit.residual_kind == "conv":
             r, rst, _ = convbn_core_forward(unit.residual, x, training)
         elif unit.residual_kind == "identity":
             r = x
         gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
-        out, xg_next = tcn_core_forward(unit.tcn1, H, training, tail=(r, rst, gm))
+        out, xg_next = tcn_core_forward(unit.tcn1, None, training, tail=(r, rst, gm),
+                                        pre=pre)
         if gm is not None:
             consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
         return out, None

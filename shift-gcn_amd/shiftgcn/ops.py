@@ -124,7 +124,24 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
     return out
 
 
-TAIL_MAX_PLANE = 16384   # sgcn_tshift_fwd_tail: LDS-staged planes only
+TAIL_MAX_PLANE = 16384   # sgcn_tshift_fwd_tail / _pre: LDS-staged planes only
+
+
+def tshift_fwd_pre(z, xpos, ypos, stride, zst, r, rst, ast):
+    """Inference: shift(ast-affine(relu(per-joint zst-affine(z) + res))) in one launch;
+    res = r or rst-affine(r). The Shift_gcn output H is never materialised."""
+    check_input(z, "z")
+    check_input(r, "residual")
+    B, C, H, W = z.shape
+    out = torch.empty((B, C, H // stride, W), device=z.device, dtype=_F32)
+    nb = 4 * (2 * z.numel() + out.numel())
+    with _timed("tshift_fwd", 0, nb, z):
+        rc = _lib.load().sgcn_tshift_fwd_pre(
+            _ptr(z), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(zst.scale), _ptr(zst.shift),
+            _ptr(r), _ptr(rst.scale) if rst else None, _ptr(rst.shift) if rst else None,
+            _ptr(ast.scale), _ptr(ast.shift), B, C, H, W, stride, 1, _stream(z))
+    _lib.check(rc, "sgcn_tshift_fwd_pre")
+    return out
 
 
 def tshift_fwd_tail(inp, xpos, ypos, stride, st, r=None, rst=None, gather_m=None):
