@@ -91,3 +91,25 @@ def test_ensemble_graph_replay_matches_eager():
         s_g, l_g = ens_graph.run(x)
         torch.cuda.synchronize()
         assert torch.equal(s_g, s_eager) and torch.equal(l_g, l_eager)
+
+
+@pytest.mark.parametrize("cin,cout,stride,residual,V", [(3, 64, 1, False, 25),
+                                                        (64, 64, 1, True, 33),
+                                                        (64, 128, 2, True, 25),
+                                                        (128, 256, 2, True, 33)])
+def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V):
+    """The no-backward recipe (Shift_gcn tail staged into shift_in, unit tail in the
+    shift_out store, next-unit gather) equals the eval recipe a backward would use."""
+    import shiftgcn
+    torch.manual_seed(3)
+    u = shiftgcn.TCN_GCN_unit(cin, cout, None, stride=stride, residual=residual,
+                              num_point=V)
+    formula.fill_state(u, seed=40 + cin + cout)
+    u = u.to(DEV).eval()
+    x = formula.tensor((3, cin, 20, V), 50 + cout, 1.0).to(DEV)
+    with torch.no_grad():
+        fused = u(x)
+    xr = x.clone().requires_grad_(True)
+    ref = u(xr).detach()
+    err = (fused - ref).abs().max().item()
+    assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
