@@ -222,6 +222,12 @@ def main():
         roof = {"bound": "mfma" if mfma else "hbm", "kernel": dom,
                 "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4),
+                # per launch max(FLOP/157.3T, bytes/8T) summed, over the measured time: the
+                # fraction of its own roofline (MFMA- or HBM-bound per launch) the class runs at
+                "roofline_time_frac": round(d["roof_ms"] / d["ms_total"], 4),
+                "timed_classes_roofline_time_frac": round(
+                    sum(v["roof_ms"] for v in summ.values()) /
+                    sum(v["ms_total"] for v in summ.values()), 4),
                 "traffic": None if traffic is None else round(traffic),
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": tsrc or None,
@@ -279,6 +285,7 @@ def _roofline(summ, n_iters, value_per_gpu, gflop_per_unit):
     return {"bound": "mfma" if mfma else "hbm", "kernel": dom,
             "achieved": round(achieved, 3), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": None,
+            "roofline_time_frac": round(d["roof_ms"] / d["ms_total"], 4),
             "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
             "launches_per_iter": d["launches"] // n_iters,
             "avg_launch_us": round(per_launch_s * 1e6, 2),

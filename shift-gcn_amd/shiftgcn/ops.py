@@ -43,15 +43,19 @@ class LaunchTimer:
         rec[4].record(torch.cuda.current_stream(rec[5]))
         self.records.append(rec[:5])
 
-    def summary(self):
-        """{op: {launches, ms_total, flops, bytes}} (call after a device sync)."""
+    def summary(self, peak_flops=157.3e12, peak_bytes=8.0e12):
+        """{op: {launches, ms_total, flops, bytes, roof_ms}} (call after a device sync);
+        roof_ms = sum over launches of max(flops / peak_flops, bytes / peak_bytes), the
+        time each launch would take at its own roofline bound."""
         out = {}
         for op, fl, nb, e0, e1 in self.records:
-            d = out.setdefault(op, {"launches": 0, "ms_total": 0.0, "flops": 0.0, "bytes": 0.0})
+            d = out.setdefault(op, {"launches": 0, "ms_total": 0.0, "flops": 0.0, "bytes": 0.0,
+                                    "roof_ms": 0.0})
             d["launches"] += 1
             d["ms_total"] += e0.elapsed_time(e1)
             d["flops"] += fl
             d["bytes"] += nb
+            d["roof_ms"] += 1e3 * max(fl / peak_flops, nb / peak_bytes)
         return out
 
 
