@@ -28,6 +28,8 @@ constexpr int kU = 4;  // elements in flight per thread per loop trip (all loads
 // part[plane] = {mean, M2} over the plane (per_joint = 0), or part[plane*V + v] over t.
 // Shifted data (x - x_first) keeps sum/sum-of-squares well conditioned; the merge over
 // the batch is done in double by bn_finalize_kernel.
+constexpr int kUM = 8;   // loads in flight per thread (a single-input reduction)
+
 template <bool PER_JOINT>
 __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restrict__ x,
                                                             float2* __restrict__ part, int T,
@@ -43,12 +45,12 @@ __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restri
     const int v = i % V, r = i / V;
     const float k0 = xp[v];      // shift: first row of this joint
     if (i < G * V) {
-      for (int t0 = r; t0 < T; t0 += G * kU) {
-        float xv[kU];
+      for (int t0 = r; t0 < T; t0 += G * kUM) {
+        float xv[kUM];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) xv[u] = xp[min(t0 + u * G, T - 1) * V + v];
+        for (int u = 0; u < kUM; ++u) xv[u] = xp[min(t0 + u * G, T - 1) * V + v];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
+        for (int u = 0; u < kUM; ++u) {
           const float d = (t0 + u * G < T) ? xv[u] - k0 : 0.f;
           a += d;
           q += d * d;
@@ -67,12 +69,12 @@ __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restri
   } else {
     const float k0 = xp[0];
     float a = 0.f, q = 0.f;
-    for (int base = 0; base < P; base += kThreads * kU) {
-      float xv[kU];
+    for (int base = 0; base < P; base += kThreads * kUM) {
+      float xv[kUM];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) xv[u] = xp[min(base + u * kThreads + i, P - 1)];
+      for (int u = 0; u < kUM; ++u) xv[u] = xp[min(base + u * kThreads + i, P - 1)];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
+      for (int u = 0; u < kUM; ++u) {
         const float d = (base + u * kThreads + i < P) ? xv[u] - k0 : 0.f;
         a += d;
         q += d * d;
