@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 8
+#define SGCN_ABI_VERSION 9
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -210,10 +210,16 @@ int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, in
 
 /* Shift_gcn input side of the backward: dx[b,c,t,v] = dxt[b,c,t,u]*m[u][c] + add1 + add2
  * with u = (v - c) mod V (transpose of the shift_in gather); dmask_part[b][c][u] =
- * sum_t dxt * x0 at the gathered position. add1/add2 may be NULL. */
+ * sum_t dxt * x0 at the gathered position. add1/add2 may be NULL.
+ * prev_part (optional, B*C float2, with prev_s/prev_mean/prev_invstd): when x0 is the
+ * output relu(bn2(prev_s) + residual) of the previous TCN_GCN_unit and dx is its complete
+ * gradient, also write that bn2's sgcn_bn_bwd_reduce partials {sum g, sum g*xhat},
+ * g = dx*(x0 > 0), xhat = (prev_s - prev_mean[c])*prev_invstd[c] — so the previous
+ * unit's backward skips its reduce pass. */
 int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
-                       const float* add2, float* dx, float* dmask_part, int B, int C, int T,
-                       int V, void* stream);
+                       const float* add2, float* dx, float* dmask_part, const float* prev_s,
+                       const float* prev_mean, const float* prev_invstd, float* prev_part,
+                       int B, int C, int T, int V, void* stream);
 
 /* dmask[u][c] (+)= (sum_b dmask_part[b][c][u]) * (1 - tanh(mask[u][c])^2). */
 int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,

@@ -490,11 +490,17 @@ __global__ __launch_bounds__(kThreads) void gcn_gather_kernel(const float* __res
 // ------------------------------------------------------------------------------------
 // dx[b,c,t,v'] = dxt[b,c,t,u]*m[u][c] (+ add1 + add2), u = (v' - c) mod V  (index_select^T)
 // dmask_part[b][c][u] = sum_t dxt[b,c,t,u] * x0[b,c,t,(u+c) mod V]
-template <bool ADD1, bool ADD2>
+// PART: also the backward partials of the PREVIOUS unit's tail BatchNorm (bn2, whose
+// output after residual + ReLU is x0): bn_part[plane] = {sum g, sum g*(s - mean)*invstd},
+// g = dx * (x0 > 0), s = that BatchNorm's input (same layout) — what sgcn_bn_bwd_reduce
+// would compute from (dx, x0, s) in another pass over three tensors.
+template <bool ADD1, bool ADD2, bool PART>
 __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
     const float* __restrict__ dxt, const float* __restrict__ x0, const float* __restrict__ m,
     const float* __restrict__ add1, const float* __restrict__ add2, float* __restrict__ dx,
-    float* __restrict__ dmask_part, int C, int T, int V) {
+    float* __restrict__ dmask_part, const float* __restrict__ ps,
+    const float* __restrict__ pmean, const float* __restrict__ pinvstd,
+    float2* __restrict__ bn_part, int C, int T, int V) {
   // One pass: thread i owns destination joint v' = i % V of rows t = i / V (mod G), so its
   // source joint u = (v' - c) mod V is fixed: one mask value, one dmask accumulator, and
   // the x0 factor of the mask gradient, x0[t, (u + c) mod V] = x0[t, v'], is the element
@@ -509,10 +515,12 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
   int us = vd - rc;
   us = us < 0 ? us + V : us;
   const float mu = m[us * C + c];
-  float acc = 0.f;
+  float pm = 0.f, pi = 0.f;
+  if (PART) { pm = pmean[c]; pi = pinvstd[c]; }
+  float acc = 0.f, b0 = 0.f, b1 = 0.f;
   if (i < G * V) {
     for (int t0 = rr; t0 < T; t0 += G * kU) {
-      float gv[kU], xq[kU], a1[kU], a2[kU];
+      float gv[kU], xq[kU], a1[kU], a2[kU], sv[kU];
 #pragma unroll
       for (int k = 0; k < kU; ++k) {
         const int row = min(t0 + k * G, T - 1) * V;
@@ -520,6 +528,7 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
         xq[k] = x0[off + row + vd];
         if (ADD1) a1[k] = add1[off + row + vd];
         if (ADD2) a2[k] = add2[off + row + vd];
+        if (PART) sv[k] = ps[off + row + vd];
       }
 #pragma unroll
       for (int k = 0; k < kU; ++k) {
@@ -529,8 +538,18 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
         if (ADD2) val += a2[k];
         if (t < T) dx[off + t * V + vd] = val;
         acc += (t < T) ? gv[k] * xq[k] : 0.f;
+        if (PART) {
+          const float g = (t < T && xq[k] > 0.f) ? val : 0.f;
+          b0 += g;
+          b1 += g * ((sv[k] - pm) * pi);
+        }
       }
     }
+  }
+  if (PART) {
+    __shared__ float red[2 * kThreads / 64];
+    block_sum2(b0, b1, red);
+    if (i == 0) bn_part[plane] = make_float2(b0, b1);
   }
   s0[i] = acc;
   __syncthreads();
@@ -746,16 +765,23 @@ int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, in
 }
 
 int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
-                       const float* add2, float* dx, float* dmask_part, int B, int C, int T,
-                       int V, void* stream) {
+                       const float* add2, float* dx, float* dmask_part, const float* prev_s,
+                       const float* prev_mean, const float* prev_invstd, float* prev_part,
+                       int B, int C, int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(dxt && x0 && m && dx && dmask_part);
+  SGCN_REQUIRE(!prev_part || (prev_s && prev_mean && prev_invstd));
   hipStream_t st = (hipStream_t)stream;
-#define SGCN_FIN(A1, A2) \
-  gcn_dx_finish_kernel<A1, A2><<<B * C, kThreads, 0, st>>>(dxt, x0, m, add1, add2, dx, dmask_part, C, T, V)
-  if (add1) { if (add2) SGCN_FIN(true, true); else SGCN_FIN(true, false); }
-  else { if (add2) SGCN_FIN(false, true); else SGCN_FIN(false, false); }
+  float2* pp = (float2*)prev_part;
+#define SGCN_FIN(A1, A2, PT)                                                                \
+  gcn_dx_finish_kernel<A1, A2, PT><<<B * C, kThreads, 0, st>>>(                           \
+      dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V)
+#define SGCN_FIN_P(A1, A2) \
+  do { if (pp) SGCN_FIN(A1, A2, true); else SGCN_FIN(A1, A2, false); } while (0)
+  if (add1) { if (add2) SGCN_FIN_P(true, true); else SGCN_FIN_P(true, false); }
+  else { if (add2) SGCN_FIN_P(false, true); else SGCN_FIN_P(false, false); }
+#undef SGCN_FIN_P
 #undef SGCN_FIN
   SGCN_LAUNCH_CHECK();
   return 0;

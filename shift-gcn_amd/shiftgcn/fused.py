@@ -82,7 +82,7 @@ def gcn_forward(mod, x0, training):
     return H, s
 
 
-def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None):
+def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, extra_out=None):
     """Returns (dx0, {param_name: grad}). With ``dy_coef`` ([3, Cout]) the incoming
     gradient is dH = k1*dH_arg + k2*H + k3 (Shift_tcn.bn's input gradient), evaluated
     on the fly by the BN-backward kernels instead of being materialised."""
@@ -117,7 +117,11 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None):
     g["Linear_weight"], g["Linear_bias"] = dLW, dLb
     dXt = _empty(B, Cin, T, V, like=x0)
     ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
-    dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=extra_dx)
+    if prev is not None:   # also the previous unit's bn2 backward partials (x0 = its out)
+        dx, mpart, extra_out["prev_part"] = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id,
+                                                              add2=extra_dx, prev=prev)
+    else:
+        dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=extra_dx)
     g["Feature_Mask"] = ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V)
     if mod.has_down:
         dWd = torch.empty_like(conv.weight)
@@ -267,7 +271,7 @@ def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate):
 # TCN_GCN_unit
 # ======================================================================================
 class UnitSaved:
-    __slots__ = ("x", "gs", "ts", "rs", "out")
+    __slots__ = ("x", "gs", "ts", "rs", "out", "prev")
 
 
 def unit_forward(unit, x, training):
@@ -288,6 +292,10 @@ def unit_forward(unit, x, training):
         if gm is not None:
             consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
         return out, None
+    # the previous unit's tail (its out is x): its bn2 backward partials are made by this
+    # unit's gcn_dx_finish, which reads x anyway (see unit_backward)
+    prev = unit.__dict__.pop("_prev_tail", None)
+    prev = prev[1:] if prev is not None and prev[0] is x else None
     H, gs = gcn_forward(unit.gcn1, x, training)
     S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
     rs = None
@@ -304,8 +312,11 @@ def unit_forward(unit, x, training):
     if gm is not None:
         out, xg_next = out
         consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
+    nxt = unit.__dict__.get("_next_unit")
+    if nxt is not None and unit.residual_kind != "conv" and nxt.residual_kind != "conv":
+        nxt.__dict__["_prev_tail"] = (out, S, sst, unit)
     s = UnitSaved()
-    s.x, s.gs, s.ts, s.rs, s.out = x, gs, ts, rs, out
+    s.x, s.gs, s.ts, s.rs, s.out, s.prev = x, gs, ts, rs, out, prev
     return out, s
 
 
@@ -315,7 +326,10 @@ def unit_backward(unit, s: UnitSaved, dout):
     B, Cout, To, V = S.shape
     kind = unit.residual_kind
     g = {}
-    if kind == "conv":
+    cached = unit.__dict__.pop("_bwd_part", None)
+    if cached is not None and cached[0] is dout and kind != "conv":
+        part, rpart = cached[1], None   # made by the next unit's gcn_dx_finish
+    elif kind == "conv":
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False, r=s.rs.Rc,
                                         rst=s.rs.rst)
     else:
@@ -337,8 +351,12 @@ def unit_backward(unit, s: UnitSaved, dout):
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dx=dS)
     (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, dS, materialize_dx=False)
     g.update({"tcn1." + k: v for k, v in gt.items()})
+    extra = {}
     dx, gg = gcn_backward(unit.gcn1, s.gs, dA, extra_dx=dres if kind == "identity" else None,
-                          dy_coef=coefA)
+                          dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
+                          extra_out=extra)
+    if s.prev is not None:   # kind != "conv": dx is final here
+        s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
     g.update({"gcn1." + k: v for k, v in gg.items()})
     if kind == "conv":
         gr = convbn_dx_and_dw(unit.residual, s.rs, dres, dx, accumulate=True)

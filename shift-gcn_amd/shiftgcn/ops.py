@@ -382,14 +382,21 @@ def gcn_gather(x0, m):
     return xg
 
 
-def gcn_dx_finish(dxt, x0, m, add1=None, add2=None):
+def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None):
+    """Returns (dx, dmask partials[, prev_part]); ``prev`` = (S, BnStats) of the previous
+    unit's bn2 adds its backward-reduce partials (see sgcn_gcn_dx_finish)."""
     B, C, T, V = dxt.shape
     dx = torch.empty_like(dxt)
     part = torch.empty((B * C * V,), device=dxt.device, dtype=_F32)
+    pp = torch.empty((B * C * 2,), device=dxt.device, dtype=_F32) if prev is not None else None
+    ps, pst = prev if prev is not None else (None, None)
     rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1), _ptr(add2),
-                                        _ptr(dx), _ptr(part), B, C, T, V, _stream(dxt))
+                                        _ptr(dx), _ptr(part), _ptr(ps),
+                                        _ptr(pst.mean) if pst else None,
+                                        _ptr(pst.invstd) if pst else None, _ptr(pp), B, C, T,
+                                        V, _stream(dxt))
     _lib.check(rc, "sgcn_gcn_dx_finish")
-    return dx, part
+    return (dx, part) if prev is None else (dx, part, pp)
 
 
 def mask_grad_finalize(part, mask, B, C, V):

@@ -202,13 +202,17 @@ class Model(nn.Module):
         units = [getattr(self, f"l{k}") for k in range(1, 11)]
         try:
             # each unit's tail launch also writes the next unit's gathered gcn input
+            # and the next unit's backward makes this unit's bn2 backward partials
             for u, nxt in zip(units[:-1], units[1:]):
                 u.__dict__["_gather_consumer"] = nxt.gcn1
+                u.__dict__["_next_unit"] = nxt
             for u in units:
                 x = u(x)
         finally:
             for u in units:
                 u.__dict__.pop("_gather_consumer", None)
+                u.__dict__.pop("_next_unit", None)
+                u.__dict__.pop("_prev_tail", None)
                 u.gcn1.__dict__.pop("_gather_cache", None)
         c_new = x.size(1)
         x = x.view(N, M, c_new, -1)
