@@ -134,9 +134,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    # Rehearsal knobs (never set by the driver): SGCN_BENCH_BACKEND=gloo and
+    # SGCN_BENCH_SAME_DEVICE=1 run N ranks on one GPU to exercise the N>1 code path.
+    backend = os.environ.get("SGCN_BENCH_BACKEND", "nccl")
+    if os.environ.get("SGCN_BENCH_SAME_DEVICE") == "1":
+        local = 0
     if distributed:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     if args.config == "ens":
         return bench_ensemble(args, dev, rank, world, distributed)
@@ -198,8 +206,10 @@ def main():
     ms = 1000.0 * elapsed / args.steps
 
     roof = None
-    if args.roofline and rank == 0:
-        # HIP events around every launch of each kernel class, over K eager steps
+    if args.roofline:
+        # HIP events around every launch of each kernel class, over K eager steps. Every
+        # rank runs these steps (they contain the gradient all-reduce, so a rank-0-only
+        # loop would wait forever for the others); rank 0 reports.
         timer = ops.LaunchTimer()
         ops.set_launch_timer(timer)
         torch.cuda.synchronize()
