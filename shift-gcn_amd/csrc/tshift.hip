@@ -782,16 +782,16 @@ void launch_bwd(bool affine, bool relu, const float* gout, const float* in, cons
 
 constexpr int kBwdThreads = 512;
 
-template <int LPT, int STRIDE>
+template <int LPT, int STRIDE, int NT = kBwdThreads>
 void launch_bwd_lds(bool affine, bool relu, const float* gout, const float* in,
                     const float* xpos, const float* ypos, const float* scale,
                     const float* shift, const float* bmu, const float* bis, float* gin,
                     float2* pg, float2* bp, int B, int C, int H, int W, int Ho, int add_half,
                     hipStream_t st) {
-  dim3 grid(B * C), block(kBwdThreads);
+  dim3 grid(B * C), block(NT);
   const size_t lds = (size_t)(STRIDE == 1 ? Ho : H + Ho) * W * sizeof(float);
 #define SGCN_BWDL(A, R, P)                                                                  \
-  tshift_bwd_lds_kernel<kBwdThreads, LPT, A, R, STRIDE, P><<<grid, block, lds, st>>>(      \
+  tshift_bwd_lds_kernel<NT, LPT, A, R, STRIDE, P><<<grid, block, lds, st>>>(               \
       gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, Ho, add_half)
   if (bp) {
     if (affine) {
@@ -964,6 +964,17 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   float2* bp = (float2*)bn_part;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
   if ((stride == 1 ? H : H + Ho) * W <= kBwdLdsMax && H > 0) {
+    if (stride == 1 && H * W <= 4096) {
+      // small planes (T = 150 / 75): 256 threads, so fewer lanes idle per workgroup
+      if (H * W <= 2048)
+        launch_bwd_lds<8, 1, 256>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st);
+      else
+        launch_bwd_lds<16, 1, 256>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st);
+      SGCN_LAUNCH_CHECK();
+      tshift_pos_finalize_kernel<<<(C + 31) / 32, 256, 0, st>>>(pg, B, C, gx, gy);
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
     const int lpt = pick_lpt(stride == 1 ? H * W : (H + Ho) * W, kBwdThreads);
 #define SGCN_BWDL_LPT(L)                                                                      \
   (stride == 1 ? launch_bwd_lds<L, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,  \
