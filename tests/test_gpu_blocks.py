@@ -227,3 +227,33 @@ def test_eval_mode_backward_matches_oracle(kind, cin, cout, stride):
     g = formula.tensor((2, cout, To, 25), 9 + cout, 1.0)
     xr, yr, xo, yo = _run_pair(ref, ours, x, g)
     _compare(ref, ours, xr, yr, xo, yo, f"eval-{kind}", train=False)
+
+
+def test_model_backward_fusion_paths_taken(monkeypatch):
+    """The cross-unit fusions are exercised by the model tests' numerics; this pins that
+    they are actually taken: the next unit's gcn_dx_finish makes the bn2 backward partials
+    of units l1, l2, l3, l6, l9 (successor without a conv residual), so only 10 per-joint
+    (gcn) + 5 unit-tail reduce passes remain; every unit but l1 gets its gathered gcn
+    input from the previous unit's tail launch (one standalone gather)."""
+    import shiftgcn
+    from shiftgcn import ops
+    counts = {"reduce": 0, "gather": 0}
+    real_reduce, real_gather = ops.bn_bwd_reduce, ops.gcn_gather
+
+    def reduce(*a, **k):
+        counts["reduce"] += 1
+        return real_reduce(*a, **k)
+
+    def gather(*a, **k):
+        counts["gather"] += 1
+        return real_gather(*a, **k)
+
+    monkeypatch.setattr(ops, "bn_bwd_reduce", reduce)
+    monkeypatch.setattr(ops, "gcn_gather", gather)
+    m = shiftgcn.Model(num_class=60, num_point=25, num_person=2,
+                       graph="graph.ntu_rgb_d.Graph").to(DEV).train()
+    x = formula.tensor((2, 3, 16, 25, 2), 5, 1.0).to(DEV)
+    m(x).sum().backward()
+    torch.cuda.synchronize()
+    assert counts["gather"] == 1, counts
+    assert counts["reduce"] == 15, counts
