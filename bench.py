@@ -48,9 +48,9 @@ PEAK_HBM_GBS = 8000.0      # HBM3E spec
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
-def pmc_traffic(op):
+def pmc_traffic(op, path=None):
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(path or PMC_TRAFFIC) as f:
             d = json.load(f)
         return d["ops"][op]["bytes_per_call"], d.get("source", "")
     except (OSError, KeyError, ValueError):
@@ -376,6 +376,11 @@ def bench_ensemble(args, dev, rank, world, distributed):
         torch.cuda.synchronize()
         ops.set_launch_timer(None)
         roof = _roofline(timer.summary(), n, value / world, GFLOP_PER_WINDOW_ENS)
+        traffic, tsrc = pmc_traffic(roof["kernel"], os.path.join(REPO, "profiles",
+                                                                 "pmc_traffic_ens.json"))
+        roof["traffic"] = None if traffic is None else round(traffic)
+        roof["traffic_unit"] = "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+        roof["traffic_source"] = tsrc or None
     cpu = cpu_baseline_ensemble() if (args.cpu_baseline and rank == 0 and world == 1) else None
     if rank == 0:
         print(json.dumps({
