@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 9
+#define SGCN_ABI_VERSION 10
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -72,6 +72,17 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
                          const float* r_scale, const float* r_shift, const float* gather_m,
                          float* out_gathered, int B, int C, int H, int W, int stride,
                          int ypos_is_raw, void* stream);
+
+/* sgcn_tshift_bwd (stride 1, ReLU mask on `in`, no affine) whose gout is the input
+ * gradient of the BatchNorm that follows the shift inside a TCN_GCN_unit (Shift_tcn.bn2,
+ * shift_gcn.py:73,161-162), formed while staging: gout = k1*(y > 0 ? dy : 0) + k2*s + k3
+ * with dy/y the unit's output gradient/output, s = bn2's input, coef = [3][C] {k1,k2,k3}
+ * from sgcn_bn_bwd_finalize. That gradient tensor is never written. H*W <= 16384 only
+ * (else SGCN_EINVAL: use sgcn_bn_bwd_apply + sgcn_tshift_bwd). */
+int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const float* coef,
+                         const float* in, const float* xpos, const float* ypos, float* gin,
+                         float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
+                         int W, int ypos_is_raw, void* stream);
 
 /* Workspace bytes for sgcn_tshift_bwd (B*C float2 plane partials). */
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
@@ -215,11 +226,13 @@ int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, in
  * output relu(bn2(prev_s) + residual) of the previous TCN_GCN_unit and dx is its complete
  * gradient, also write that bn2's sgcn_bn_bwd_reduce partials {sum g, sum g*xhat},
  * g = dx*(x0 > 0), xhat = (prev_s - prev_mean[c])*prev_invstd[c] — so the previous
- * unit's backward skips its reduce pass. */
+ * unit's backward skips its reduce pass. add2_mask (optional, needs add1 and add2): add2
+ * enters as add2 * (add2_mask > 0) (a unit's identity-residual gradient dout*(out > 0),
+ * formed here rather than written by the unit tail's BatchNorm backward). */
 int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
-                       const float* add2, float* dx, float* dmask_part, const float* prev_s,
-                       const float* prev_mean, const float* prev_invstd, float* prev_part,
-                       int B, int C, int T, int V, void* stream);
+                       const float* add2, const float* add2_mask, float* dx, float* dmask_part,
+                       const float* prev_s, const float* prev_mean, const float* prev_invstd,
+                       float* prev_part, int B, int C, int T, int V, void* stream);
 
 /* dmask[u][c] (+)= (sum_b dmask_part[b][c][u]) * (1 - tanh(mask[u][c])^2). */
 int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,

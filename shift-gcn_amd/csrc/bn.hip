@@ -494,13 +494,16 @@ __global__ __launch_bounds__(kThreads) void gcn_gather_kernel(const float* __res
 // output after residual + ReLU is x0): bn_part[plane] = {sum g, sum g*(s - mean)*invstd},
 // g = dx * (x0 > 0), s = that BatchNorm's input (same layout) — what sgcn_bn_bwd_reduce
 // would compute from (dx, x0, s) in another pass over three tensors.
-template <bool ADD1, bool ADD2, bool PART>
+// A2M: add2 enters masked, add2 * (add2m > 0) — the identity-residual gradient of a
+// TCN_GCN_unit, g = dout * (out > 0), formed here instead of being written by the tail's
+// BatchNorm backward.
+template <bool ADD1, bool ADD2, bool PART, bool A2M = false>
 __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
     const float* __restrict__ dxt, const float* __restrict__ x0, const float* __restrict__ m,
     const float* __restrict__ add1, const float* __restrict__ add2, float* __restrict__ dx,
     float* __restrict__ dmask_part, const float* __restrict__ ps,
     const float* __restrict__ pmean, const float* __restrict__ pinvstd,
-    float2* __restrict__ bn_part, int C, int T, int V) {
+    float2* __restrict__ bn_part, int C, int T, int V, const float* __restrict__ add2m) {
   // One pass: thread i owns destination joint v' = i % V of rows t = i / V (mod G), so its
   // source joint u = (v' - c) mod V is fixed: one mask value, one dmask accumulator, and
   // the x0 factor of the mask gradient, x0[t, (u + c) mod V] = x0[t, v'], is the element
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
   float acc = 0.f, b0 = 0.f, b1 = 0.f;
   if (i < G * V) {
     for (int t0 = rr; t0 < T; t0 += G * kU) {
-      float gv[kU], xq[kU], a1[kU], a2[kU], sv[kU];
+      float gv[kU], xq[kU], a1[kU], a2[kU], sv[kU], a2q[kU];
 #pragma unroll
       for (int k = 0; k < kU; ++k) {
         const int row = min(t0 + k * G, T - 1) * V;
@@ -528,6 +531,7 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
         xq[k] = x0[off + row + vd];
         if (ADD1) a1[k] = add1[off + row + vd];
         if (ADD2) a2[k] = add2[off + row + vd];
+        if (A2M) a2q[k] = add2m[off + row + vd];
         if (PART) sv[k] = ps[off + row + vd];
       }
 #pragma unroll
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
         const int t = t0 + k * G;
         float val = gv[k] * mu;
         if (ADD1) val += a1[k];
-        if (ADD2) val += a2[k];
+        if (ADD2) val += A2M ? (a2q[k] > 0.f ? a2[k] : 0.f) : a2[k];
         if (t < T) dx[off + t * V + vd] = val;
         acc += (t < T) ? gv[k] * xq[k] : 0.f;
         if (PART) {
@@ -765,18 +769,33 @@ int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, in
 }
 
 int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
-                       const float* add2, float* dx, float* dmask_part, const float* prev_s,
-                       const float* prev_mean, const float* prev_invstd, float* prev_part,
-                       int B, int C, int T, int V, void* stream) {
+                       const float* add2, const float* add2_mask, float* dx, float* dmask_part,
+                       const float* prev_s, const float* prev_mean, const float* prev_invstd,
+                       float* prev_part, int B, int C, int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(dxt && x0 && m && dx && dmask_part);
   SGCN_REQUIRE(!prev_part || (prev_s && prev_mean && prev_invstd));
+  SGCN_REQUIRE(!add2_mask || add2);
   hipStream_t st = (hipStream_t)stream;
   float2* pp = (float2*)prev_part;
+  if (add2_mask) {   // the identity-unit form: add1 given, add2 masked by add2_mask
+    SGCN_REQUIRE(add1);
+    if (pp)
+      gcn_dx_finish_kernel<true, true, true, true><<<B * C, kThreads, 0, st>>>(
+          dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,
+          add2_mask);
+    else
+      gcn_dx_finish_kernel<true, true, false, true><<<B * C, kThreads, 0, st>>>(
+          dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,
+          add2_mask);
+    SGCN_LAUNCH_CHECK();
+    return 0;
+  }
 #define SGCN_FIN(A1, A2, PT)                                                                \
   gcn_dx_finish_kernel<A1, A2, PT><<<B * C, kThreads, 0, st>>>(                           \
-      dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V)
+      dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,  \
+      nullptr)
 #define SGCN_FIN_P(A1, A2) \
   do { if (pp) SGCN_FIN(A1, A2, true); else SGCN_FIN(A1, A2, false); } while (0)
   if (add1) { if (add2) SGCN_FIN_P(true, true); else SGCN_FIN_P(true, false); }

@@ -517,14 +517,22 @@ __global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
   }
 }
 
-template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP>
+// GP (stride 1 only): gout is not read; it is the input gradient of the BatchNorm that
+// follows this shift (Shift_tcn.bn2 inside a TCN_GCN_unit, shift_gcn.py:73,161-162),
+// formed while staging: gout = k1*(gy > 0 ? gdy : 0) + k2*gx + k3 (gdy = the unit's output
+// gradient, gy = its output, gx = bn2's input S, k = sgcn_bn_bwd_finalize coefficients),
+// so that gradient tensor is never written.
+template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP, bool GP = false>
 __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
     float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
-    int Hb, int W, int Ho, int add_half) {
+    int Hb, int W, int Ho, int add_half, const float* __restrict__ gdy = nullptr,
+    const float* __restrict__ gy = nullptr, const float* __restrict__ gx = nullptr,
+    const float* __restrict__ gcoef = nullptr) {
+  static_assert(!GP || STRIDE == 1, "GP is a stride-1 (re-associated) variant");
   // STRIDE == 1 ("re-associated"): only gout is staged (half the LDS -> twice the
   // workgroups per CU); each thread's own input elements are loaded into registers with
   // the staging loads, and the position-gradient sums are accumulated over INPUT positions
@@ -551,10 +559,26 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ go = gout + (size_t)plane * nt;
     const float* __restrict__ src = in + (size_t)plane * nb;
     float t[LPT];
+    if (GP) {
+      const size_t po = (size_t)plane * nt;
+      const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
+      float u1[LPT], u2[LPT];
 #pragma unroll
-    for (int e = 0; e < LPT; ++e) {
-      t[e] = go[min(e * NT + (int)threadIdx.x, nt - 1)];
-      rin_r[e] = src[min(e * NT + (int)threadIdx.x, nb - 1)];
+      for (int e = 0; e < LPT; ++e) {
+        const int i = min(e * NT + (int)threadIdx.x, nt - 1);
+        t[e] = gdy[po + i];
+        u1[e] = gy[po + i];
+        u2[e] = gx[po + i];
+        rin_r[e] = src[min(e * NT + (int)threadIdx.x, nb - 1)];
+      }
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
+    } else {
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) {
+        t[e] = go[min(e * NT + (int)threadIdx.x, nt - 1)];
+        rin_r[e] = src[min(e * NT + (int)threadIdx.x, nb - 1)];
+      }
     }
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
@@ -939,6 +963,34 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
   }
 #undef SGCN_TAIL_RG
 #undef SGCN_TAIL
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const float* coef,
+                         const float* in, const float* xpos, const float* ypos, float* gin,
+                         float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
+                         int W, int ypos_is_raw, void* stream) {
+  SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0);
+  SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
+  SGCN_REQUIRE(dy && y && s && coef && in && xpos && ypos && gin && gx && gy && ws);
+  SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
+  SGCN_REQUIRE((long long)B * C < (1LL << 31));
+  (void)ypos_is_raw;   // stride 1: the +0.5 of shift.py:17-18 never applies
+  hipStream_t st = (hipStream_t)stream;
+  float2* pg = (float2*)ws;
+  const size_t lds = (size_t)H * W * sizeof(float);
+#define SGCN_BNIN(NT, L)                                                                       \
+  tshift_bwd_lds_kernel<NT, L, false, true, 1, false, true><<<B * C, NT, lds, st>>>(           \
+      nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, C, H, W, \
+      H, 0, dy, y, s, coef)
+  if (H * W <= 2048) SGCN_BNIN(256, 8);
+  else if (H * W <= 4096) SGCN_BNIN(256, 16);
+  else if (H * W <= 8192) SGCN_BNIN(512, 16);
+  else SGCN_BNIN(512, 32);
+#undef SGCN_BNIN
+  SGCN_LAUNCH_CHECK();
+  tshift_pos_finalize_kernel<<<(C + 31) / 32, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

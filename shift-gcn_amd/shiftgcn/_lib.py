@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen: one HIP runtime per proces
 
 LIB_NAME = "libshiftgcn_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 9
+ABI_VERSION = 10
 EINVAL = -22
 
 _lib = None
@@ -55,8 +55,10 @@ SIGNATURES = {
                                _P]),
     "sgcn_mask_prep": (_I, [_P, _P, _I, _P]),
     "sgcn_gcn_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
-    "sgcn_gcn_dx_finish": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
-                                _P]),
+    "sgcn_gcn_dx_finish": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,
+                                _I, _P]),
+    "sgcn_tshift_bwd_bnin": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
+                                  _I, _I, _P]),
     "sgcn_mask_grad_finalize": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "sgcn_modalities": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
 }

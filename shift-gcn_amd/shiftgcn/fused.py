@@ -117,11 +117,13 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     g["Linear_weight"], g["Linear_bias"] = dLW, dLb
     dXt = _empty(B, Cin, T, V, like=x0)
     ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
+    a2, a2m = extra_dx if isinstance(extra_dx, tuple) else (extra_dx, None)
     if prev is not None:   # also the previous unit's bn2 backward partials (x0 = its out)
         dx, mpart, extra_out["prev_part"] = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id,
-                                                              add2=extra_dx, prev=prev)
+                                                              add2=a2, prev=prev,
+                                                              add2_mask=a2m)
     else:
-        dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=extra_dx)
+        dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
     g["Feature_Mask"] = ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V)
     if mod.has_down:
         dWd = torch.empty_like(conv.weight)
@@ -201,7 +203,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
     return S, sst, s
 
 
-def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True):
+def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None):
     """dS: gradient w.r.t. S (pre-bn2). Returns (dH, grads), or ((dA, coef), grads) with
     ``materialize_dx=False`` (dH = coef[0]*dA + coef[1]*H + coef[2], fused downstream)."""
     H = s.H
@@ -209,8 +211,12 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True):
     Cout = mod.out_channels
     si, so = mod.shift_in, mod.shift_out
     g = {}
-    dRp, g["shift_out.xpos"], g["shift_out.ypos"] = ops.tshift_bwd(
-        dS, s.R, so.xpos.detach(), so.ypos.detach(), so.stride, relu_mask=True)
+    if gpre is not None:   # dS = bn2's input gradient, formed inside the shift backward
+        dRp, g["shift_out.xpos"], g["shift_out.ypos"] = ops.tshift_bwd_bnin(
+            gpre[0], gpre[1], s.S, gpre[2], s.R, so.xpos.detach(), so.ypos.detach())
+    else:
+        dRp, g["shift_out.xpos"], g["shift_out.ypos"] = ops.tshift_bwd(
+            dS, s.R, so.xpos.detach(), so.ypos.detach(), so.stride, relu_mask=True)
     tl = mod.temporal_linear
     dWt = torch.empty_like(tl.weight)
     dbt = torch.empty_like(tl.bias)
@@ -336,6 +342,22 @@ def unit_backward(unit, s: UnitSaved, dout):
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False)
     coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
         part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
+    if (kind != "conv" and unit.tcn1.shift_out.stride == 1 and
+            S.shape[2] * S.shape[3] <= ops.BNIN_MAX_PLANE):
+        # neither dS nor the identity-residual gradient is written: the shift_out backward
+        # forms dS while staging, gcn_dx_finish forms dout*(out > 0)
+        (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, None, materialize_dx=False,
+                                            gpre=(dout, s.out, coef2))
+        g.update({"tcn1." + k: v for k, v in gt.items()})
+        extra = {}
+        dx, gg = gcn_backward(unit.gcn1, s.gs, dA,
+                              extra_dx=(dout, s.out) if kind == "identity" else None,
+                              dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
+                              extra_out=extra)
+        if s.prev is not None:
+            s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
+        g.update({"gcn1." + k: v for k, v in gg.items()})
+        return dx, g
     dS = torch.empty_like(S)
     dres = None
     if kind == "conv":

@@ -199,6 +199,29 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     return gin, gx, gy
 
 
+BNIN_MAX_PLANE = 16384   # sgcn_tshift_bwd_bnin: LDS-staged stride-1 planes only
+
+
+def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos):
+    """Stride-1 shift backward (ReLU mask on ``inp``) whose output gradient is the input
+    gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3, formed in the
+    kernel. Returns (grad_input, grad_xpos, grad_ypos)."""
+    B, C, H, W = inp.shape
+    lib = _lib.load()
+    dev = inp.device
+    gin = torch.empty_like(inp)
+    gx = torch.empty((C,), device=dev, dtype=_F32)
+    gy = torch.empty((C,), device=dev, dtype=_F32)
+    nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
+    ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
+    with _timed("tshift_bwd", 0, 4 * (3 * dy.numel() + 2 * inp.numel()), inp):
+        rc = lib.sgcn_tshift_bwd_bnin(_ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp),
+                                      _ptr(xpos), _ptr(ypos), _ptr(gin), _ptr(gx), _ptr(gy),
+                                      _ptr(ws), nbytes, B, C, H, W, 1, _stream(inp))
+    _lib.check(rc, "sgcn_tshift_bwd_bnin")
+    return gin, gx, gy
+
+
 # --------------------------------------------------------------------------------------
 # pointwise (1x1) contraction with fused joint-shift gathers
 # --------------------------------------------------------------------------------------
@@ -382,7 +405,7 @@ def gcn_gather(x0, m):
     return xg
 
 
-def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None):
+def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
     """Returns (dx, dmask partials[, prev_part]); ``prev`` = (S, BnStats) of the previous
     unit's bn2 adds its backward-reduce partials (see sgcn_gcn_dx_finish)."""
     B, C, T, V = dxt.shape
@@ -391,7 +414,7 @@ def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None):
     pp = torch.empty((B * C * 2,), device=dxt.device, dtype=_F32) if prev is not None else None
     ps, pst = prev if prev is not None else (None, None)
     rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1), _ptr(add2),
-                                        _ptr(dx), _ptr(part), _ptr(ps),
+                                        _ptr(add2_mask), _ptr(dx), _ptr(part), _ptr(ps),
                                         _ptr(pst.mean) if pst else None,
                                         _ptr(pst.invstd) if pst else None, _ptr(pp), B, C, T,
                                         V, _stream(dxt))
