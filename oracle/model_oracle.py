@@ -57,7 +57,11 @@ class ShiftFunction(torch.autograd.Function):
 
 
 class Shift(nn.Module):
-    """``shift.py:32-46``: owns per-channel ``xpos``/``ypos``."""
+    """``shift.py:32-46``: owns per-channel ``xpos``/``ypos``. ``function`` is the autograd
+    Function standing in for ``ShiftFunction`` (the numpy restatement by default; the
+    full-size GPU parity tests swap in a torch-on-device restatement)."""
+
+    function = ShiftFunction
 
     def __init__(self, channel, stride, init_scale=3):
         super().__init__()
@@ -68,7 +72,7 @@ class Shift(nn.Module):
         self.ypos.data.uniform_(-init_scale, init_scale)
 
     def forward(self, x):
-        return ShiftFunction.apply(x, self.xpos, self.ypos, self.stride)
+        return self.function.apply(x, self.xpos, self.ypos, self.stride)
 
 
 # --------------------------------------------------------------------------------------

@@ -38,8 +38,10 @@ F32 = np.float32
 
 
 def _floor_int(v: np.ndarray) -> np.ndarray:
-    """``int x1 = floorf(x)`` (.cu:49) on a float vector."""
-    return np.floor(v).astype(np.int64)
+    """``int x1 = floorf(x)`` (.cu:49) on a float vector. ``floorf`` is the float function:
+    a double ``x`` (the reference's AT_DISPATCH double instantiation, .cu:413) is rounded
+    to float first."""
+    return np.floor(v.astype(np.float32)).astype(np.int64)
 
 
 def _taps(plane: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.ndarray:
@@ -59,13 +61,31 @@ def _taps(plane: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.ndarray:
     return np.where(valid[None], out, plane.dtype.type(0)).astype(plane.dtype)
 
 
-def _bilinear(q11, q21, q12, q22, dx, dy):
+def _fma(a, b, c):
+    """fma(a, b, c) in the operands' precision: the float32 product is exact in float64,
+    the sum is rounded in float64 and then to float32 (a double rounding that can differ
+    from a true fused multiply-add in the last bit of rare ties; the contracted variant is
+    only used as a bound, never for bit-exact checks)."""
+    dt = np.result_type(a, b, c)
+    if dt == np.float64:
+        return a * b + c            # no wider type to emulate with; bound use only
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(dt)
+
+
+def _bilinear(q11, q21, q12, q22, dx, dy, contract=False):
     """``q11*(1-dx)*(1-dy) + q21*dx*(1-dy) + q12*(1-dx)*dy + q22*dx*dy`` (.cu:73),
-    evaluated left to right in float32 (each product/sum rounded once)."""
+    evaluated left to right in float32 (each product/sum rounded once).
+
+    ``contract=True``: the FMA-contracted evaluation nvcc emits by default
+    (``--fmad=true``): each ``+ (u*v)*w`` becomes ``fma(u*v, w, acc)``."""
     one = q11.dtype.type(1)
     omdx = one - dx
     omdy = one - dy
     t1 = (q11 * omdx) * omdy
+    if contract:
+        acc = _fma(q21 * dx, omdy, t1)
+        acc = _fma(q12 * omdx, dy, acc)
+        return _fma(q22 * dx, dy, acc).astype(q11.dtype)
     t2 = (q21 * dx) * omdy
     t3 = (q12 * omdx) * dy
     t4 = (q22 * dx) * dy
@@ -79,9 +99,11 @@ def _frac(pos: np.ndarray):
     return i1, d
 
 
-def shift_forward(inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray, stride: int) -> np.ndarray:
+def shift_forward(inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray, stride: int,
+                  contract: bool = False) -> np.ndarray:
     """Forward temporal shift. ``ypos`` must already carry the +0.5 for stride != 1
-    (``shift.py:17-18``). Output shape (B, C, H // stride, W) (.cu:408)."""
+    (``shift.py:17-18``). Output shape (B, C, H // stride, W) (.cu:408).
+    ``contract``: FMA-contracted blend (see :func:`_bilinear`)."""
     inp = np.ascontiguousarray(inp)
     dt = inp.dtype
     B, C, H, W = inp.shape
@@ -100,7 +122,7 @@ def shift_forward(inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray, stride: i
     q22 = _taps(inp, hy2, wx2)
     dxb = dx[None, :, None, None]
     dyb = dy[None, :, None, None]
-    return _bilinear(q11, q21, q12, q22, dxb, dyb)
+    return _bilinear(q11, q21, q12, q22, dxb, dyb, contract)
 
 
 def _taps_stride2_top(gout: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.ndarray:
@@ -122,7 +144,7 @@ def _taps_stride2_top(gout: np.ndarray, hh: np.ndarray, ww: np.ndarray) -> np.nd
 
 
 def shift_bottom_backward(gout: np.ndarray, xpos: np.ndarray, ypos: np.ndarray,
-                          H: int, stride: int) -> np.ndarray:
+                          H: int, stride: int, contract: bool = False) -> np.ndarray:
     """Input gradient: bilinear sample of ``grad_output`` at the reversed position
     ``(-xpos, -ypos)`` over the bottom grid (.cu:78-152 stride 1, .cu:155-256 stride 2)."""
     gout = np.ascontiguousarray(gout)
@@ -146,11 +168,12 @@ def shift_bottom_backward(gout: np.ndarray, xpos: np.ndarray, ypos: np.ndarray,
     q21 = tap(gout, hy1, wx2)
     q12 = tap(gout, hy2, wx1)
     q22 = tap(gout, hy2, wx2)
-    return _bilinear(q11, q21, q12, q22, dx[None, :, None, None], dy[None, :, None, None])
+    return _bilinear(q11, q21, q12, q22, dx[None, :, None, None], dy[None, :, None, None],
+                     contract)
 
 
 def shift_position_backward(inp: np.ndarray, gout: np.ndarray, xpos: np.ndarray,
-                            ypos: np.ndarray, stride: int):
+                            ypos: np.ndarray, stride: int, contract: bool = False):
     """Per-output-element position gradients ``val_x*g`` and ``val_y*g`` (.cu:277-363).
 
     Returns the two (B, C, Ho, W) temporaries the reference materialises (.cu:480-481)."""
@@ -175,8 +198,13 @@ def shift_position_backward(inp: np.ndarray, gout: np.ndarray, xpos: np.ndarray,
     dxb = dx[None, :, None, None]
     dyb = dy[None, :, None, None]
     # val_x = (1-dy)*(q21-q11)+dy*(q22-q12); val_y = (1-dx)*(q12-q11)+dx*(q22-q21)  (.cu:343-344)
-    val_x = ((one - dyb) * (q21 - q11) + dyb * (q22 - q12)).astype(dt)
-    val_y = ((one - dxb) * (q12 - q11) + dxb * (q22 - q21)).astype(dt)
+    if contract:   # nvcc --fmad=true: a*b + c*d -> fma(c, d, a*b)
+        val_x = _fma(np.broadcast_to(dyb, q22.shape), q22 - q12, (one - dyb) * (q21 - q11))
+        val_y = _fma(np.broadcast_to(dxb, q22.shape), q22 - q21, (one - dxb) * (q12 - q11))
+        val_x, val_y = val_x.astype(dt), val_y.astype(dt)
+    else:
+        val_x = ((one - dyb) * (q21 - q11) + dyb * (q22 - q12)).astype(dt)
+        val_y = ((one - dxb) * (q12 - q11) + dxb * (q22 - q21)).astype(dt)
     return (val_x * gout).astype(dt), (val_y * gout).astype(dt)
 
 
@@ -209,12 +237,13 @@ def apply_shift_constraint(gx: np.ndarray, gy: np.ndarray):
 
 
 def shift_backward(gout: np.ndarray, inp: np.ndarray, xpos: np.ndarray, ypos: np.ndarray,
-                   stride: int):
+                   stride: int, contract: bool = False):
     """``shift_cuda_backward`` (.cu:433-523): returns ``(grad_input, grad_xpos, grad_ypos)``.
-    ``ypos`` is the (possibly +0.5-shifted) value saved by the forward (``shift.py:21``)."""
+    ``ypos`` is the (possibly +0.5-shifted) value saved by the forward (``shift.py:21``).
+    ``contract``: the FMA-contracted variant of .cu:73 / .cu:343-344 (nvcc's default)."""
     H = inp.shape[2]
-    gin = shift_bottom_backward(gout, xpos, ypos, H, stride)
-    gxb, gyb = shift_position_backward(inp, gout, xpos, ypos, stride)
+    gin = shift_bottom_backward(gout, xpos, ypos, H, stride, contract)
+    gxb, gyb = shift_position_backward(inp, gout, xpos, ypos, stride, contract)
     gx, gy = apply_shift_constraint(reduce_position_grad(gxb), reduce_position_grad(gyb))
     return gin, gx, gy
 

@@ -29,27 +29,63 @@ def is_shift_position(name: str) -> bool:
     return name.endswith(".xpos") or name.endswith(".ypos") or name in ("xpos", "ypos")
 
 
+def trainable_named(model: torch.nn.Module):
+    """The parameters that take part in the reduction (the int64 ``shift_in``/``shift_out``
+    index arrays are ``requires_grad=False`` and never get a gradient)."""
+    return [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+
+
+def reduction_scale(named, world: int, shift_grad_rule: str = "sum") -> torch.Tensor:
+    """Per-element factor applied to the all-reduced SUM of the flat gradient bucket:
+    ``1/world`` for ordinary parameters (DataParallel's sum of replica gradients of the
+    global-mean loss == mean of per-rank local-mean-loss gradients, equal shards) and 1 for
+    shift positions under the default ``"sum"`` rule (DataParallel reduce-adds each
+    replica's already sign-normalised +-0.01, ``_functions.py:31-32``)."""
+    if shift_grad_rule not in ("sum", "mean"):
+        raise ValueError(shift_grad_rule)
+    total = sum(p.numel() for _, p in named)
+    scale = torch.empty(total, dtype=torch.float32)
+    off = 0
+    for n, p in named:
+        k = p.numel()
+        keep_sum = is_shift_position(n) and shift_grad_rule == "sum"
+        scale[off:off + k] = 1.0 if keep_sum else 1.0 / world
+        off += k
+    return scale
+
+
+def combine_local(grads_per_rank, named, shift_grad_rule: str = "sum"):
+    """What :class:`GradAllReduce` leaves in every rank's ``.grad`` given each rank's local
+    gradients (a list over ranks of {name: grad}), computed in one process: the SUM over
+    ranks (rank order) times :func:`reduction_scale`. Used to check a set of shard passes
+    against the DataParallel emulation without a process group."""
+    world = len(grads_per_rank)
+    scale = reduction_scale(named, world, shift_grad_rule)
+    flat = None
+    for g in grads_per_rank:
+        f = torch.cat([g[n].reshape(-1).float().cpu() for n, _ in named])
+        flat = f if flat is None else flat + f
+    flat = flat * scale
+    out, off = {}, 0
+    for n, p in named:
+        k = p.numel()
+        out[n] = flat[off:off + k].view(p.shape)
+        off += k
+    return out
+
+
 class GradAllReduce:
     """Callable run between ``backward()`` and ``optimizer.step()``."""
 
     def __init__(self, model: torch.nn.Module, group=None, shift_grad_rule: str = "sum"):
-        if shift_grad_rule not in ("sum", "mean"):
-            raise ValueError(shift_grad_rule)
         self.group = group
         self.world = dist.get_world_size(group)
-        self.named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        self.named = trainable_named(model)
         dev = self.named[0][1].device
-        sizes = [p.numel() for _, p in self.named]
-        self.total = sum(sizes)
-        scale = torch.empty(self.total, dtype=torch.float32)
-        off = 0
-        for (n, p), k in zip(self.named, sizes):
-            keep_sum = is_shift_position(n) and shift_grad_rule == "sum"
-            scale[off:off + k] = 1.0 if keep_sum else 1.0 / self.world
-            off += k
-        self.scale = scale.to(dev)
+        self.sizes = [p.numel() for _, p in self.named]
+        self.total = sum(self.sizes)
+        self.scale = reduction_scale(self.named, self.world, shift_grad_rule).to(dev)
         self.flat = torch.zeros(self.total, dtype=torch.float32, device=dev)
-        self.sizes = sizes
 
     def __call__(self):
         grads = []

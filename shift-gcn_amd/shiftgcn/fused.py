@@ -319,7 +319,11 @@ def unit_forward(unit, x, training):
         out, xg_next = out
         consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
     nxt = unit.__dict__.get("_next_unit")
-    if nxt is not None and unit.residual_kind != "conv" and nxt.residual_kind != "conv":
+    # the next unit's gcn_dx_finish may produce this unit's bn2 backward partials only if
+    # the dx it reads is this unit's COMPLETE output gradient: no residual conv (whose dx is
+    # added after) and no gcn down conv (whose dx is accumulated after gcn_dx_finish)
+    if (nxt is not None and unit.residual_kind != "conv" and nxt.residual_kind != "conv"
+            and not nxt.gcn1.has_down):
         nxt.__dict__["_prev_tail"] = (out, S, sst, unit)
     s = UnitSaved()
     s.x, s.gs, s.ts, s.rs, s.out, s.prev = x, gs, ts, rs, out, prev
@@ -377,7 +381,7 @@ def unit_backward(unit, s: UnitSaved, dout):
     dx, gg = gcn_backward(unit.gcn1, s.gs, dA, extra_dx=dres if kind == "identity" else None,
                           dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
                           extra_out=extra)
-    if s.prev is not None:   # kind != "conv": dx is final here
+    if s.prev is not None:   # kind != "conv" and no gcn down conv: dx is final here
         s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
     g.update({"gcn1." + k: v for k, v in gg.items()})
     if kind == "conv":
@@ -395,7 +399,14 @@ def trainable(module):
 
 class _BlockFunction(torch.autograd.Function):
     """Generic Function: ``fwd(module, x, training) -> (y, saved)`` and
-    ``bwd(module, saved, dy) -> (dx, {param_name: grad})``."""
+    ``bwd(module, saved, dy) -> (dx, {param_name: grad})``.
+
+    The block's input and output are registered with ``save_for_backward`` so autograd's
+    version counters guard them: an in-place op on either between forward and backward
+    (e.g. ``y.relu_()``) raises autograd's usual "modified by an inplace operation" error
+    instead of silently corrupting the ReLU-mask / BatchNorm backward. The fused recipe's
+    other saved activations are private (never returned) and are released after the first
+    backward; a second backward through the same graph raises a clear error."""
 
     @staticmethod
     def forward(ctx, impl, module, x, *params):
@@ -404,12 +415,19 @@ class _BlockFunction(torch.autograd.Function):
         y, saved = fwd(module, x.contiguous(), training)
         ctx.impl, ctx.module, ctx.saved, ctx.training = impl, module, saved, training
         ctx.names = [n for n, _ in trainable(module)]
+        ctx.save_for_backward(x, y)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         # eval-mode blocks back-propagate through their running-statistics BatchNorms
         # (fixed affine maps); the BnStats objects saved by the forward carry the mode
+        ctx.saved_tensors   # version check of the block's input and output
+        if ctx.saved is None:
+            raise RuntimeError(
+                f"{type(ctx.module).__name__}: backward through the fused HIP block was "
+                "called a second time; its saved activations are released after the first "
+                "backward (retain_graph=True / double backward is not supported)")
         _, bwd = ctx.impl
         dx, grads = bwd(ctx.module, ctx.saved, dy.contiguous())
         ctx.saved = None

@@ -240,6 +240,32 @@ class PlaneView:
         self.rsign = rsign
 
 
+# The contraction kernels address each operand through a 32-bit buffer descriptor: every
+# plane operand's extent must stay below 2^29 elements (sgcn_pw_fwd / sgcn_pw_dw return
+# SGCN_EINVAL otherwise, pwconv.hip). Larger batches (NTU l5 at > ~279 clips per GPU) are
+# split over B here into chunks that fit; the result is identical (forward/dX: every output
+# element is the same fixed-order sum) or the same deterministic split-K reduction
+# accumulated chunk by chunk (dW).
+PW_MAX_ELEMS = 1 << 29
+
+
+def _plane_extent(v: PlaneView, B, C, T, V):
+    return (B - 1) * v.bstride + C * v.cstride + T * v.tstride * V
+
+
+def _batch_chunk(views, B, T, V):
+    """Largest batch chunk whose every (view, channels) extent is < PW_MAX_ELEMS."""
+    bc = B
+    for v, C in views:
+        per = v.bstride
+        fixed = C * v.cstride + T * v.tstride * V
+        if fixed >= PW_MAX_ELEMS:
+            raise ValueError("pointwise operand plane too large for one sample")
+        if (B - 1) * per + fixed >= PW_MAX_ELEMS:
+            bc = min(bc, max(1, (PW_MAX_ELEMS - 1 - fixed) // max(per, 1) + 1))
+    return bc
+
+
 def pw_fwd(w, w_mcontig, bias, x: PlaneView, out: PlaneView, M, K, T, V, mask=None,
            relu=False, accumulate=False):
     check_input(w, "weight")
@@ -247,12 +273,17 @@ def pw_fwd(w, w_mcontig, bias, x: PlaneView, out: PlaneView, M, K, T, V, mask=No
     B = x.t.shape[0]
     lib = _lib.load()
     P = B * T * V
+    bc = _batch_chunk([(x, K), (out, M)], B, T, V)
     with _timed("pw_fwd", 2.0 * P * M * K, 4.0 * P * (M * (2 if accumulate else 1) + K), x.t):
-        rc = lib.sgcn_pw_fwd(_ptr(w), int(w_mcontig), _ptr(bias), _ptr(x.t), x.bstride,
-                             x.cstride, x.tstride, x.rsign, _ptr(mask), _ptr(out.t),
-                             out.bstride, out.cstride, out.tstride, out.rsign, int(relu),
-                             int(accumulate), B, M, K, T, V, _stream(x.t))
-    _lib.check(rc, "sgcn_pw_fwd")
+        for b0 in range(0, B, bc):
+            nb = min(bc, B - b0)
+            rc = lib.sgcn_pw_fwd(_ptr(w), int(w_mcontig), _ptr(bias),
+                                 x.t.data_ptr() + 4 * b0 * x.bstride, x.bstride,
+                                 x.cstride, x.tstride, x.rsign, _ptr(mask),
+                                 out.t.data_ptr() + 4 * b0 * out.bstride,
+                                 out.bstride, out.cstride, out.tstride, out.rsign, int(relu),
+                                 int(accumulate), nb, M, K, T, V, _stream(x.t))
+            _lib.check(rc, "sgcn_pw_fwd")
     return out.t
 
 
@@ -262,16 +293,21 @@ def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=Fals
     _opt(dbias, "dbias"), _opt(mask, "mask")
     B = g.t.shape[0]
     lib = _lib.load()
-    nbytes = lib.sgcn_pw_dw_ws_bytes(B, M, Nc, T, V)
+    bc = _batch_chunk([(g, M), (x, Nc)], B, T, V)
+    nbytes = lib.sgcn_pw_dw_ws_bytes(bc, M, Nc, T, V)
     ws = torch.empty((nbytes + 3) // 4, device=g.t.device, dtype=_F32)
     P = B * T * V
     with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t):
-        rc = lib.sgcn_pw_dw(_ptr(g.t), g.bstride, g.cstride, g.tstride, g.rsign, _ptr(x.t),
-                            x.bstride, x.cstride, x.tstride, x.rsign, _ptr(mask), _ptr(dw),
-                            int(transpose), int(accumulate), _ptr(dbias),
-                            int(dbias_accumulate), _ptr(ws), nbytes, B, M, Nc, T, V,
-                            _stream(g.t))
-    _lib.check(rc, "sgcn_pw_dw")
+        for b0 in range(0, B, bc):
+            nb = min(bc, B - b0)
+            first = b0 == 0
+            rc = lib.sgcn_pw_dw(g.t.data_ptr() + 4 * b0 * g.bstride, g.bstride, g.cstride,
+                                g.tstride, g.rsign, x.t.data_ptr() + 4 * b0 * x.bstride,
+                                x.bstride, x.cstride, x.tstride, x.rsign, _ptr(mask),
+                                _ptr(dw), int(transpose), int(accumulate or not first),
+                                _ptr(dbias), int(dbias_accumulate or not first), _ptr(ws),
+                                nbytes, nb, M, Nc, T, V, _stream(g.t))
+            _lib.check(rc, "sgcn_pw_dw")
     return dw
 
 

@@ -13,6 +13,7 @@ instantiated by ``Model``) uses ``torch.nn.functional.conv2d`` on the device.
 """
 from __future__ import annotations
 
+import contextlib
 import importlib
 import math
 
@@ -200,21 +201,29 @@ class Model(nn.Module):
         """Body + head of ``forward`` (shift_gcn.py:200-216) on an input already permuted
         to (N*M, C, T, V) and normalised by ``data_bn`` (e.g. by ``sgcn_modalities``)."""
         units = [getattr(self, f"l{k}") for k in range(1, 11)]
-        try:
-            # each unit's tail launch also writes the next unit's gathered gcn input
-            # and the next unit's backward makes this unit's bn2 backward partials
-            for u, nxt in zip(units[:-1], units[1:]):
-                u.__dict__["_gather_consumer"] = nxt.gcn1
-                u.__dict__["_next_unit"] = nxt
+        with linked_units(units):
             for u in units:
                 x = u(x)
-        finally:
-            for u in units:
-                u.__dict__.pop("_gather_consumer", None)
-                u.__dict__.pop("_next_unit", None)
-                u.__dict__.pop("_prev_tail", None)
-                u.gcn1.__dict__.pop("_gather_cache", None)
         c_new = x.size(1)
         x = x.view(N, M, c_new, -1)
         x = x.mean(3).mean(1)
         return self.fc(x)
+
+
+@contextlib.contextmanager
+def linked_units(units):
+    """Run a chain of TCN_GCN_units with the cross-unit fusions on (what Model.forward
+    does for l1..l10): each unit's tail launch also writes the next unit's gathered gcn
+    input, and the next unit's backward makes this unit's bn2 backward partials. The links
+    live only for the duration of the block (a unit used alone runs unfused)."""
+    try:
+        for u, nxt in zip(units[:-1], units[1:]):
+            u.__dict__["_gather_consumer"] = nxt.gcn1
+            u.__dict__["_next_unit"] = nxt
+        yield
+    finally:
+        for u in units:
+            u.__dict__.pop("_gather_consumer", None)
+            u.__dict__.pop("_next_unit", None)
+            u.__dict__.pop("_prev_tail", None)
+            u.gcn1.__dict__.pop("_gather_cache", None)

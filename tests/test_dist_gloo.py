@@ -4,10 +4,16 @@ Checks the nn.DataParallel-equivalent reduction rule of shiftgcn.dist.GradAllRed
 (SURVEY §8e): ordinary parameter gradients are MEANED over ranks (== DataParallel's sum
 of replica grads of the global-mean loss), shift-position gradients (xpos/ypos, already
 sign-normalised per replica) are SUMMED; BN running stats are taken from rank 0.
+
+``test_real_model_*`` run the REAL parameter set (the CPU oracle of ``model/shift_gcn.py``:
+693,107 trainable parameters incl. 20x2 shift-position vectors, 50 BatchNorms, the int64
+index parameters) through GradAllReduce on two half-batches and compare with the
+single-process DataParallel restatement (``oracle/dp_oracle.py``, main.py:294-299).
 """
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -88,3 +94,99 @@ def test_scale_vector_single_process(rule):
     from shiftgcn.dist import is_shift_position
     assert is_shift_position("l1.tcn1.shift_in.ypos") and is_shift_position("a.xpos")
     assert not is_shift_position("l1.gcn1.Linear_weight")
+
+
+# --------------------------------------------------------------------------------------
+# the real model (oracle restatement of model/shift_gcn.py) through GradAllReduce
+# --------------------------------------------------------------------------------------
+REAL = dict(N=4, T=24, V=25, M=2, num_class=60, seed=123)
+
+
+def _real_inputs():
+    import formula
+    x = formula.tensor((REAL["N"], 3, REAL["T"], REAL["V"], REAL["M"]), 77, 1.0)
+    labels = torch.arange(REAL["N"]) * 7 % REAL["num_class"]
+    return x, labels
+
+
+def _real_model():
+    import formula
+    from oracle import model_oracle as mo
+    m = mo.Model(num_class=REAL["num_class"], num_point=REAL["V"], num_person=REAL["M"])
+    formula.fill_state(m, seed=REAL["seed"])
+    return m.train()
+
+
+def _real_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    from conftest import GOLDEN, REPO
+    for p in (REPO, GOLDEN):
+        sys.path.insert(0, p)
+    torch.set_num_threads(1)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shiftgcn.dist import GradAllReduce, broadcast_buffers, broadcast_parameters
+        m = _real_model()
+        broadcast_parameters(m)
+        x, labels = _real_inputs()
+        n = x.shape[0] // world
+        xs, ls = x[rank * n:(rank + 1) * n], labels[rank * n:(rank + 1) * n]
+        loss = torch.nn.functional.cross_entropy(m(xs), ls)    # local-mean loss per rank
+        m.zero_grad(set_to_none=True)
+        loss.backward()
+        GradAllReduce(m)()
+        broadcast_buffers(m)
+        # numpy across the queue (tensor storages would be fd-shared with an exiting process)
+        q.put((rank, {k: p.grad.numpy().copy() for k, p in m.named_parameters()
+                      if p.requires_grad},
+               {k: b.numpy().copy() for k, b in m.named_buffers()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_real_model_grad_allreduce_equals_dataparallel_gloo_world2():
+    """Two gloo ranks x half batch == nn.DataParallel(k=2) on the whole batch, bit for bit:
+    the local-mean CE gradient is exactly 2x the replica's global-mean one (a power of two),
+    so sum-then-halve reproduces DataParallel's replica sum exactly; xpos/ypos are the SUM
+    of the per-rank +-0.01; every rank ends with replica 0's BN running statistics."""
+    from oracle.dp_oracle import dataparallel_grads
+    res = _spawn(_real_worker)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        ref = _real_model()
+        x, labels = _real_inputs()
+        _, _, g_dp = dataparallel_grads(ref, x, labels, 2)
+    finally:
+        torch.set_num_threads(prev)
+    n_shift = 0
+    for rank, grads, bufs in res:
+        assert set(grads) == set(g_dp)
+        for k, g in grads.items():
+            gd = g_dp[k].numpy()
+            assert np.array_equal(g, gd), (rank, k, float(np.abs(g - gd).max()))
+            if k.endswith("ypos"):
+                # the sum of two sign-normalised replica grads: 0 or +-0.02
+                vals = set(np.round(g / 0.01).astype(int).tolist())
+                assert vals <= {-2, 0, 2}, (k, vals)
+                n_shift += 1
+        for k, b in ref.named_buffers():
+            assert np.array_equal(bufs[k], b.numpy()), (rank, k)
+    assert n_shift == 2 * 20   # 2 ranks x 10 units x (shift_in, shift_out)

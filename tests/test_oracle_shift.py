@@ -110,3 +110,52 @@ def test_oracle_matches_reference_glue_fixture(golden, case):
 def test_effective_ypos_is_torch_fp32_add():
     y = np.array([0.1, -0.3, 1e-8, 2.5, -0.5], F32)
     assert np.array_equal(so.effective_ypos(y, 2), (torch.from_numpy(y) + 0.5).numpy())
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_fma_contracted_variant_is_within_one_rounding(stride):
+    """The FMA-contracted restatement (nvcc --fmad=true of .cu:73, .cu:343-344) differs from
+    the uncontracted one only by rounding: forward / input gradient within 1e-6 relative to
+    the tensor scale (well inside the 1e-5 bar), identical constrained position grads up
+    to sign flips of near-zero plane sums."""
+    rng = np.random.default_rng(11 + stride)
+    B, C, H, W = 2, 8, 40, 25
+    x = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    xpos = rng.uniform(-1e-8, 1e-8, C).astype(np.float32)
+    ypos = so.effective_ypos(rng.uniform(-3, 3, C).astype(np.float32), stride)
+    g = rng.standard_normal((B, C, H // stride, W)).astype(np.float32)
+    a = so.shift_forward(x, xpos, ypos, stride)
+    b = so.shift_forward(x, xpos, ypos, stride, contract=True)
+    assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max()
+    ga, gxa, gya = so.shift_backward(g, x, xpos, ypos, stride)
+    gb, gxb, gyb = so.shift_backward(g, x, xpos, ypos, stride, contract=True)
+    assert np.abs(ga - gb).max() <= 1e-6 * np.abs(ga).max()
+    assert (gya != gyb).sum() <= 1 and (gxa != gxb).sum() <= 1
+    # integer shifts (dx = dy = 0): contraction cannot change a pure translation
+    yi = np.round(ypos).astype(np.float32)
+    assert np.array_equal(so.shift_forward(x, np.zeros_like(xpos), yi, 1),
+                          so.shift_forward(x, np.zeros_like(xpos), yi, 1, contract=True))
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_torch_restatement_matches_numpy_oracle(stride):
+    """tests/torch_shift.py (the on-device eager reference of the full-size parity tests)
+    agrees with the numpy oracle on the CPU."""
+    import torch_shift as ts
+    rng = np.random.default_rng(5 + stride)
+    B, C, H, W = 2, 8, 30, 25
+    x = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    xpos = rng.uniform(-1e-8, 1e-8, C).astype(np.float32)
+    xpos[1] = 1.5
+    ypos = so.effective_ypos(rng.uniform(-3, 3, C).astype(np.float32), stride)
+    ypos[2] = float(H + 2)
+    g = rng.standard_normal((B, C, H // stride, W)).astype(np.float32)
+    out = ts.shift_forward(torch.from_numpy(x), torch.from_numpy(xpos), torch.from_numpy(ypos),
+                           stride).numpy()
+    ref = so.shift_forward(x, xpos, ypos, stride)
+    assert np.abs(out - ref).max() <= 1e-6 * np.abs(ref).max()
+    gin, gx, gy = ts.shift_backward(torch.from_numpy(g), torch.from_numpy(x),
+                                    torch.from_numpy(xpos), torch.from_numpy(ypos), stride)
+    rgin, rgx, rgy = so.shift_backward(g, x, xpos, ypos, stride)
+    assert np.abs(gin.numpy() - rgin).max() <= 1e-6 * np.abs(rgin).max()
+    assert (gy.numpy() != rgy).sum() <= 1 and (gx.numpy() != rgx).sum() <= 1
