@@ -46,6 +46,9 @@ PEAK_HBM_GBS = 8000.0      # HBM3E spec
 # HBM bytes per C-ABI call of each op class from the committed rocprofv3 PMC passes
 # (tools/pmc_traffic.sh + tools/pmc_summary.py --json) of this code version
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
+# per-config PMC files (the NTU figures must never be quoted on another workload)
+PMC_TRAFFIC_BY_CONFIG = {"ntu": PMC_TRAFFIC,
+                         "mp": os.path.join(REPO, "profiles", "pmc_traffic_mp.json")}
 
 
 def pmc_traffic(op, path=None):
@@ -73,18 +76,33 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, seconds_budget=30.0):
-    """The oracle (PyTorch-eager CPU restatement of the reference model) on a bounded
-    sample: 2 clips of the same workload, one fwd+bwd+SGD iteration per sample."""
-    from oracle import model_oracle as mo
-    num_class, V, M, T, _ = CONFIGS[cfg]
+def host_threads():
+    """(threads used, affinity cores): every core of this process's CPU share. The GPU box
+    grants each GPU a share of the host (OMP_NUM_THREADS, 16 per GPU there) while
+    sched_getaffinity shows the whole machine, so the share caps the affinity set."""
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
+        aff = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    n = aff if not share or not share.isdigit() else max(1, min(aff, int(share)))
+    return n, aff
+
+
+def cpu_baseline(cfg, seconds_budget=30.0):
+    """The oracle (PyTorch-eager CPU restatement of the reference model with the naive
+    torch-gather temporal shift, oracle/torch_shift.py) on the host cores, bounded samples
+    of the same workload:
+      * the metric's unit: 2 clips fwd+bwd+SGD (median of 3 after 1 warm-up);
+      * BASELINE config 1: NTU bs=2 forward only (median of >= 5 after 1 warm-up)."""
+    from oracle import model_oracle as mo
+    from oracle import torch_shift as ts
+    num_class, V, M, T, _ = CONFIGS[cfg]
+    threads, ncpu = host_threads()
     prev = torch.get_num_threads()
+    prev_fn = mo.Shift.function
     torch.set_num_threads(threads)
+    mo.Shift.function = ts.TorchShiftFunction    # torch.gather shift (config 1's fallback)
     try:
         torch.manual_seed(1)
         model = mo.Model(num_class=num_class, num_point=V, num_person=M, graph="unused").train()
@@ -110,6 +128,25 @@ def cpu_baseline(cfg, seconds_budget=30.0):
             times.append(time.perf_counter() - t0)
         times.sort()
         med = times[len(times) // 2]
+        # BASELINE config 1: NTU x-sub joint, bs=2, Model forward on CPU PyTorch eager
+        fwd = None
+        if cfg == "ntu":
+            model.eval()
+            with torch.no_grad():
+                model(x)
+                ft = []
+                t_all = time.perf_counter()
+                while len(ft) < 5 or (len(ft) < 7 and time.perf_counter() - t_all < 10):
+                    t0 = time.perf_counter()
+                    model(x)
+                    ft.append(time.perf_counter() - t0)
+            model.train()
+            ft.sort()
+            fmed = ft[len(ft) // 2]
+            fwd = {"value": round(n / fmed, 4), "unit": "clips/s", "s_per_iter": round(fmed, 4),
+                   "runs": len(ft), "cores": threads,
+                   "sample": "BASELINE config 1: NTU bs=2 (2,3,300,25,2) Model forward "
+                             "(eval, no_grad), median of runs after 1 warm-up"}
         model_name = ""
         try:
             with open("/proc/cpuinfo") as f:
@@ -123,9 +160,12 @@ def cpu_baseline(cfg, seconds_budget=30.0):
                 "kind": "port",
                 "sample": f"{cfg.upper()} bs={n} (2 clips of the bs=64 workload), fwd+bwd+SGD, "
                           f"median of {len(times)} after 1 warm-up, {med:.2f} s/iter; "
-                          f"{model_name}"}
+                          f"{threads} threads = this process's CPU share ({ncpu} cores in "
+                          f"its affinity set); {model_name}",
+                "config1_forward": fwd}
     finally:
         torch.set_num_threads(prev)
+        mo.Shift.function = prev_fn
 
 
 def main():
@@ -213,10 +253,16 @@ def main():
         timer = ops.LaunchTimer()
         ops.set_launch_timer(timer)
         torch.cuda.synchronize()
-        for _ in range(max(1, min(args.steps, 5))):
+        n_meas = max(1, min(args.steps, 5))
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record()
+        for _ in range(n_meas):
             step()
+        s1.record()
         torch.cuda.synchronize()
         ops.set_launch_timer(None)
+        step_ms_meas = s0.elapsed_time(s1) / n_meas
         summ = timer.summary()
         dom = max(summ, key=lambda k: summ[k]["ms_total"])
         d = summ[dom]
@@ -228,7 +274,7 @@ def main():
         else:
             achieved = d["bytes"] / d["launches"] / per_launch_s / 1e9
             peak, unit = PEAK_HBM_GBS, "GB/s"
-        traffic, tsrc = pmc_traffic(dom)
+        traffic, tsrc = pmc_traffic(dom, PMC_TRAFFIC_BY_CONFIG.get(args.config))
         roof = {"bound": "mfma" if mfma else "hbm", "kernel": dom,
                 "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4),
@@ -242,10 +288,17 @@ def main():
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": tsrc or None,
                 "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
-                "launches_per_step": d["launches"] // max(1, min(args.steps, 5)),
+                "launches_per_step": d["launches"] // n_meas,
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
-                "step_breakdown_ms": {k: round(v["ms_total"] / max(1, min(args.steps, 5)), 3)
+                "step_breakdown_ms": {k: round(v["ms_total"] / n_meas, 3)
                                       for k, v in sorted(summ.items())},
+                # HIP events around every C-ABI launch vs events around the whole step (same
+                # steps): the rest is torch's head/loss/optimizer kernels and launch gaps
+                "step_ms_event_timed": round(step_ms_meas, 3),
+                "step_other_ms": round(step_ms_meas - sum(v["ms_total"] for v in summ.values())
+                                       / n_meas, 3),
+                "breakdown_coverage": round(sum(v["ms_total"] for v in summ.values())
+                                            / n_meas / step_ms_meas, 4),
                 "whole_step_frac_of_fp32_peak": round(
                     value / world * GFLOP_PER_CLIP[args.config] / 1e3 / PEAK_FP32_TFLOPS, 4)}
 
@@ -310,10 +363,13 @@ def cpu_baseline_ensemble(seconds_budget=30.0):
     PyTorch eager on the host cores) on a bounded sample of 2 windows."""
     from oracle import ensemble_oracle as eo
     from oracle import model_oracle as mo
+    from oracle import torch_shift as ts
     from shiftgcn.ensemble import MEDIAPIPE_BONE_PAIRS
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, _ = host_threads()
     prev = torch.get_num_threads()
+    prev_fn = mo.Shift.function
     torch.set_num_threads(threads)
+    mo.Shift.function = ts.TorchShiftFunction
     try:
         torch.manual_seed(1)
         models = {s: mo.Model(num_class=2, num_point=33, num_person=1, graph="unused").eval()
@@ -330,6 +386,7 @@ def cpu_baseline_ensemble(seconds_budget=30.0):
                           f"as inference_pipeline.py:355-366, {dt:.2f} s"}
     finally:
         torch.set_num_threads(prev)
+        mo.Shift.function = prev_fn
 
 
 def bench_ensemble(args, dev, rank, world, distributed):

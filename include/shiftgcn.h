@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 10
+#define SGCN_ABI_VERSION 11
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -108,6 +108,19 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
                     const float* bn_mean, const float* bn_invstd, float* bn_part, float* gin,
                     float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                     int W, int stride, int ypos_is_raw, void* stream);
+
+/* Double-precision forward / backward of the temporal shift: the reference's double
+ * instantiation (AT_DISPATCH_FLOATING_TYPES, shift_cuda_kernel.cu:413, :455-520), e.g. for
+ * gradcheck of the input gradient. Same arguments and semantics as sgcn_tshift_fwd /
+ * sgcn_tshift_bwd without the fused options; `int x1 = floorf(x)` rounds the double x to
+ * float first, exactly as the reference. Workspace: sgcn_tshift_bwd_f64_ws_bytes(B, C). */
+int sgcn_tshift_fwd_f64(const double* in, double* out, const double* xpos, const double* ypos,
+                        int B, int C, int H, int W, int stride, int ypos_is_raw, void* stream);
+size_t sgcn_tshift_bwd_f64_ws_bytes(int B, int C);
+int sgcn_tshift_bwd_f64(const double* gout, const double* in, const double* xpos,
+                        const double* ypos, double* gin, double* gx, double* gy, void* ws,
+                        size_t ws_bytes, int B, int C, int H, int W, int stride,
+                        int ypos_is_raw, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Pointwise (1x1) channel contraction with the joint-shift gathers fused (fp32 MFMA)

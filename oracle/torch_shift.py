@@ -1,5 +1,7 @@
 """Torch-eager, device-agnostic restatement of the reference temporal shift (TEST
-INFRASTRUCTURE ONLY; the full-size parity tests run it on the GPU beside the HIP path).
+INFRASTRUCTURE ONLY: the full-size parity tests run it on the GPU beside the HIP path, and
+bench.py's cpu_baseline runs the oracle model with it on the host cores — BASELINE
+config 1's "naive torch.gather temporal-shift fallback").
 
 It is ``shift_cuda_kernel.cu`` written with whole-tensor gathers (the "naive torch.gather
 temporal-shift fallback" of BASELINE config 1), on whatever device/dtype its inputs have:

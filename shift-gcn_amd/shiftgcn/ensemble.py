@@ -72,10 +72,12 @@ def derive_modalities(joint, parent, planes=False, data_bn=None, out=None):
         if not planes:
             raise ValueError("data_bn is applied in the plane layout only")
         scale, shift = data_bn
-    rc = _lib.load().sgcn_modalities(
-        joint.data_ptr(), parent.data_ptr(), *[o.data_ptr() for o in out],
-        None if scale is None else scale.data_ptr(), None if shift is None else shift.data_ptr(),
-        int(planes), N, C, T, V, M, ops._stream(joint))
+    with ops._timed("modalities", 0, 4 * joint.numel() * 5, joint):
+        rc = _lib.load().sgcn_modalities(
+            joint.data_ptr(), parent.data_ptr(), *[o.data_ptr() for o in out],
+            None if scale is None else scale.data_ptr(),
+            None if shift is None else shift.data_ptr(),
+            int(planes), N, C, T, V, M, ops._stream(joint))
     _lib.check(rc, "sgcn_modalities")
     return out
 

@@ -86,14 +86,15 @@ def _stream(t: torch.Tensor):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def check_input(t: torch.Tensor, name: str) -> None:
-    """``CHECK_INPUT`` of shift_cuda.cpp:15-17 (+ dtype: the HIP path is fp32)."""
+def check_input(t: torch.Tensor, name: str, dtype=_F32) -> None:
+    """``CHECK_INPUT`` of shift_cuda.cpp:15-17 (+ dtype: the fused path is fp32; the plain
+    temporal shift also takes float64, like the reference's AT_DISPATCH_FLOATING_TYPES)."""
     if not t.is_cuda:
         raise RuntimeError(f"{name} must be a CUDA tensor")
     if not t.is_contiguous():
         raise RuntimeError(f"{name} must be contiguous")
-    if t.dtype != _F32:
-        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    if t.dtype != dtype:
+        raise RuntimeError(f"{name} must be {dtype} (got {t.dtype})")
 
 
 def _opt(t, name):
@@ -110,7 +111,11 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
     """Forward shift of ``inp`` (B,C,H,W) -> (B,C,H//stride,W). ``ypos`` is the RAW
     parameter (the +0.5 for stride != 1 is applied in-kernel). Optional fused
     per-channel input affine (scale, shift) and per-plane output moments ``stats``
-    (B*C*2 floats)."""
+    (B*C*2 floats). float64 tensors run the double-precision kernel (no fused options)."""
+    if inp.dtype == torch.float64:
+        if scale is not None or shift is not None or stats is not None:
+            raise RuntimeError("the fused shift options are float32-only")
+        return _tshift_fwd_f64(inp, xpos, ypos, stride, ypos_is_raw, out)
     check_input(inp, "input")
     check_input(xpos, "xpos")
     check_input(ypos, "ypos")
@@ -126,6 +131,43 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
                                  int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_fwd")
     return out
+
+
+def _tshift_fwd_f64(inp, xpos, ypos, stride, ypos_is_raw, out=None):
+    _F64 = torch.float64
+    check_input(inp, "input", _F64)
+    check_input(xpos, "xpos", _F64)
+    check_input(ypos, "ypos", _F64)
+    B, C, H, W = inp.shape
+    if out is None:
+        out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F64)
+    with _timed("tshift_fwd", 0, 8 * (inp.numel() + out.numel()), inp):
+        rc = _lib.load().sgcn_tshift_fwd_f64(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), B,
+                                             C, H, W, stride, int(ypos_is_raw), _stream(inp))
+    _lib.check(rc, "sgcn_tshift_fwd_f64")
+    return out
+
+
+def _tshift_bwd_f64(gout, inp, xpos, ypos, stride, ypos_is_raw):
+    _F64 = torch.float64
+    check_input(gout, "grad_output", _F64)
+    check_input(inp, "input", _F64)
+    check_input(xpos, "xpos", _F64)
+    check_input(ypos, "ypos", _F64)
+    B, C, H, W = inp.shape
+    lib = _lib.load()
+    dev = inp.device
+    gin = torch.empty_like(inp)
+    gx = torch.empty((C,), device=dev, dtype=_F64)
+    gy = torch.empty((C,), device=dev, dtype=_F64)
+    nbytes = lib.sgcn_tshift_bwd_f64_ws_bytes(B, C)
+    ws = torch.empty((max(nbytes, 8) + 7) // 8, device=dev, dtype=_F64)
+    with _timed("tshift_bwd", 0, 8 * (gout.numel() + 2 * inp.numel()), inp):
+        rc = lib.sgcn_tshift_bwd_f64(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos), _ptr(gin),
+                                     _ptr(gx), _ptr(gy), _ptr(ws), nbytes, B, C, H, W, stride,
+                                     int(ypos_is_raw), _stream(inp))
+    _lib.check(rc, "sgcn_tshift_bwd_f64")
+    return gin, gx, gy
 
 
 TAIL_MAX_PLANE = 16384   # sgcn_tshift_fwd_tail / _pre: LDS-staged planes only
@@ -170,7 +212,12 @@ def tshift_fwd_tail(inp, xpos, ypos, stride, st, r=None, rst=None, gather_m=None
 def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=False,
                ypos_is_raw=True, bn_stats=None):
     """Backward shift: returns (grad_input, grad_xpos, grad_ypos), plus the BatchNorm
-    backward partials of ``bn_stats`` (the BN whose output feeds the shift) if given."""
+    backward partials of ``bn_stats`` (the BN whose output feeds the shift) if given.
+    float64 tensors run the double-precision kernel (no fused options)."""
+    if inp.dtype == torch.float64:
+        if (scale is not None or shift is not None or relu_mask or bn_stats is not None):
+            raise RuntimeError("the fused shift options are float32-only")
+        return _tshift_bwd_f64(gout, inp, xpos, ypos, stride, ypos_is_raw)
     check_input(gout, "grad_output")
     check_input(inp, "input")
     check_input(xpos, "xpos")
@@ -318,7 +365,9 @@ def moments(x, per_joint):
     check_input(x, "input")
     B, C, T, V = x.shape
     part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=x.device, dtype=_F32)
-    rc = _lib.load().sgcn_moments(_ptr(x), _ptr(part), B, C, T, V, int(per_joint), _stream(x))
+    with _timed("bn_stats", 0, 4 * x.numel(), x):
+        rc = _lib.load().sgcn_moments(_ptr(x), _ptr(part), B, C, T, V, int(per_joint),
+                                      _stream(x))
     _lib.check(rc, "sgcn_moments")
     return part
 
@@ -342,23 +391,25 @@ def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
     lib = _lib.load()
     track = training and bn.track_running_stats and bn.running_mean is not None
     momentum = bn.momentum if bn.momentum is not None else 0.0
-    rc = lib.sgcn_bn_finalize(
-        _ptr(part), B, F, n_part, perm_V, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps),
-        float(momentum), _ptr(bn.running_mean) if track else None,
-        _ptr(bn.running_var) if track else None,
-        _ptr(bn.num_batches_tracked) if track else None, _ptr(st.mean), _ptr(st.invstd),
-        _ptr(st.scale), _ptr(st.shift), _stream(part))
+    with _timed("finalize", 0, 4 * part.numel(), part):
+        rc = lib.sgcn_bn_finalize(
+            _ptr(part), B, F, n_part, perm_V, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps),
+            float(momentum), _ptr(bn.running_mean) if track else None,
+            _ptr(bn.running_var) if track else None,
+            _ptr(bn.num_batches_tracked) if track else None, _ptr(st.mean), _ptr(st.invstd),
+            _ptr(st.scale), _ptr(st.shift), _stream(part))
     _lib.check(rc, "sgcn_bn_finalize")
     return st
 
 
 def bn_eval_coef(bn, F, perm_V=0, device=None):
     st = BnStats(F, bn.running_mean.device, batch=False)
-    rc = _lib.load().sgcn_bn_eval_coef(F, perm_V, _ptr(bn.weight), _ptr(bn.bias),
-                                       _ptr(bn.running_mean), _ptr(bn.running_var),
-                                       float(bn.eps), _ptr(st.mean), _ptr(st.invstd),
-                                       _ptr(st.scale), _ptr(st.shift),
-                                       _stream(bn.running_mean))
+    with _timed("finalize", 0, 4 * 8 * F, bn.running_mean):
+        rc = _lib.load().sgcn_bn_eval_coef(F, perm_V, _ptr(bn.weight), _ptr(bn.bias),
+                                           _ptr(bn.running_mean), _ptr(bn.running_var),
+                                           float(bn.eps), _ptr(st.mean), _ptr(st.invstd),
+                                           _ptr(st.scale), _ptr(st.shift),
+                                           _stream(bn.running_mean))
     _lib.check(rc, "sgcn_bn_eval_coef")
     return st
 
@@ -374,10 +425,14 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
     y = torch.empty_like(x) if out is None else out
     ys = torch.empty((B * C * 2,), device=x.device, dtype=_F32) if out_stats else None
     yg = torch.empty_like(y) if gather_m is not None else None
-    rc = _lib.load().sgcn_bn_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift), int(per_joint),
-                                   _ptr(r), _ptr(rst.scale) if rst else None,
-                                   _ptr(rst.shift) if rst else None, int(relu), _ptr(y),
-                                   _ptr(ys), _ptr(gather_m), _ptr(yg), B, C, T, V, _stream(x))
+    nb = 4 * x.numel() * (2 + (r is not None) + (yg is not None))
+    with _timed("bn_apply", 0, nb, x):
+        rc = _lib.load().sgcn_bn_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift),
+                                       int(per_joint), _ptr(r),
+                                       _ptr(rst.scale) if rst else None,
+                                       _ptr(rst.shift) if rst else None, int(relu), _ptr(y),
+                                       _ptr(ys), _ptr(gather_m), _ptr(yg), B, C, T, V,
+                                       _stream(x))
     _lib.check(rc, "sgcn_bn_apply")
     if gather_m is not None:
         return y, yg
@@ -391,11 +446,13 @@ def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats =
     dev = x.device
     part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=dev, dtype=_F32)
     rpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if r is not None else None
-    rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(st.mean),
-                                        _ptr(st.invstd), int(per_joint), _ptr(r),
-                                        _ptr(rst.mean) if rst else None,
-                                        _ptr(rst.invstd) if rst else None, _ptr(dy_coef),
-                                        _ptr(part), _ptr(rpart), B, C, T, V, _stream(x))
+    nb = 4 * x.numel() * (2 + (y is not None) + (r is not None))
+    with _timed("bn_bwd_reduce", 0, nb, x):
+        rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x),
+                                            _ptr(st.mean), _ptr(st.invstd), int(per_joint),
+                                            _ptr(r), _ptr(rst.mean) if rst else None,
+                                            _ptr(rst.invstd) if rst else None, _ptr(dy_coef),
+                                            _ptr(part), _ptr(rpart), B, C, T, V, _stream(x))
     _lib.check(rc, "sgcn_bn_bwd_reduce")
     return part, rpart
 
@@ -406,10 +463,11 @@ def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
     coef = torch.empty((3, F), device=dev, dtype=_F32)
     dgamma = torch.empty_like(bn.weight) if bn.weight is not None else None
     dbeta = torch.empty_like(bn.bias) if bn.bias is not None else None
-    rc = _lib.load().sgcn_bn_bwd_finalize(_ptr(part), B, F, int(n_total), perm_V,
-                                          _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
-                                          _ptr(dgamma), _ptr(dbeta), 0, int(st.batch),
-                                          _ptr(coef), _stream(part))
+    with _timed("finalize", 0, 4 * part.numel(), part):
+        rc = _lib.load().sgcn_bn_bwd_finalize(_ptr(part), B, F, int(n_total), perm_V,
+                                              _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
+                                              _ptr(dgamma), _ptr(dbeta), 0, int(st.batch),
+                                              _ptr(coef), _stream(part))
     _lib.check(rc, "sgcn_bn_bwd_finalize")
     return coef, dgamma, dbeta
 
@@ -418,9 +476,12 @@ def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, d
                  dy_coef=None):
     B, C, T, V = x.shape
     dx = torch.empty_like(x) if dx is None else dx
-    rc = _lib.load().sgcn_bn_bwd_apply(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(coef),
-                                       int(per_joint), _ptr(r), _ptr(rcoef), _ptr(dy_coef),
-                                       _ptr(dx), _ptr(dr), B, C, T, V, _stream(x))
+    nb = 4 * x.numel() * (3 + (y is not None) + (r is not None) + (dr is not None))
+    with _timed("bn_bwd_apply", 0, nb, x):
+        rc = _lib.load().sgcn_bn_bwd_apply(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(coef),
+                                           int(per_joint), _ptr(r), _ptr(rcoef),
+                                           _ptr(dy_coef), _ptr(dx), _ptr(dr), B, C, T, V,
+                                           _stream(x))
     _lib.check(rc, "sgcn_bn_bwd_apply")
     return dx
 
@@ -428,7 +489,8 @@ def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, d
 def mask_prep(mask):
     check_input(mask, "Feature_Mask")
     m = torch.empty_like(mask)
-    rc = _lib.load().sgcn_mask_prep(_ptr(mask), _ptr(m), mask.numel(), _stream(mask))
+    with _timed("finalize", 0, 8 * mask.numel(), mask):
+        rc = _lib.load().sgcn_mask_prep(_ptr(mask), _ptr(m), mask.numel(), _stream(mask))
     _lib.check(rc, "sgcn_mask_prep")
     return m
 
@@ -436,7 +498,9 @@ def mask_prep(mask):
 def gcn_gather(x0, m):
     B, C, T, V = x0.shape
     xg = torch.empty_like(x0)
-    rc = _lib.load().sgcn_gcn_gather(_ptr(x0), _ptr(m), _ptr(xg), B, C, T, V, _stream(x0))
+    with _timed("gcn_gather", 0, 8 * x0.numel(), x0):
+        rc = _lib.load().sgcn_gcn_gather(_ptr(x0), _ptr(m), _ptr(xg), B, C, T, V,
+                                         _stream(x0))
     _lib.check(rc, "sgcn_gcn_gather")
     return xg
 
@@ -449,18 +513,21 @@ def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
     part = torch.empty((B * C * V,), device=dxt.device, dtype=_F32)
     pp = torch.empty((B * C * 2,), device=dxt.device, dtype=_F32) if prev is not None else None
     ps, pst = prev if prev is not None else (None, None)
-    rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1), _ptr(add2),
-                                        _ptr(add2_mask), _ptr(dx), _ptr(part), _ptr(ps),
-                                        _ptr(pst.mean) if pst else None,
-                                        _ptr(pst.invstd) if pst else None, _ptr(pp), B, C, T,
-                                        V, _stream(dxt))
+    nb = 4 * dxt.numel() * (3 + sum(t is not None for t in (add1, add2, add2_mask, ps)))
+    with _timed("gcn_dx_finish", 0, nb, dxt):
+        rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1),
+                                            _ptr(add2), _ptr(add2_mask), _ptr(dx), _ptr(part),
+                                            _ptr(ps), _ptr(pst.mean) if pst else None,
+                                            _ptr(pst.invstd) if pst else None, _ptr(pp), B, C,
+                                            T, V, _stream(dxt))
     _lib.check(rc, "sgcn_gcn_dx_finish")
     return (dx, part) if prev is None else (dx, part, pp)
 
 
 def mask_grad_finalize(part, mask, B, C, V):
     dmask = torch.empty_like(mask)
-    rc = _lib.load().sgcn_mask_grad_finalize(_ptr(part), _ptr(mask), B, C, V, _ptr(dmask), 0,
-                                             _stream(mask))
+    with _timed("finalize", 0, 4 * part.numel(), mask):
+        rc = _lib.load().sgcn_mask_grad_finalize(_ptr(part), _ptr(mask), B, C, V, _ptr(dmask),
+                                                 0, _stream(mask))
     _lib.check(rc, "sgcn_mask_grad_finalize")
     return dmask

@@ -11,7 +11,7 @@ import torch
 from torch.autograd import Function
 from torch.nn import Module, Parameter
 
-from . import ops
+from . import torch_ops  # noqa: F401  (registers torch.ops.shiftgcn.tshift_fwd / _bwd)
 
 
 class ShiftFunction(Function):
@@ -27,7 +27,8 @@ class ShiftFunction(Function):
     @staticmethod
     def forward(ctx, input, xpos, ypos, stride=1):  # noqa: A002 (reference name)
         input = input.contiguous()
-        output = ops.tshift_fwd(input, xpos.detach(), ypos.detach(), stride)
+        output = torch.ops.shiftgcn.tshift_fwd(input, xpos.detach(), ypos.detach(), stride,
+                                               True)
         ctx.save_for_backward(input, xpos, ypos)
         ctx.stride = stride
         return output
@@ -36,8 +37,8 @@ class ShiftFunction(Function):
     def backward(ctx, grad_output):
         grad_output = grad_output.contiguous()
         input, xpos, ypos = ctx.saved_tensors
-        gin, gx, gy = ops.tshift_bwd(grad_output, input, xpos.detach(), ypos.detach(),
-                                     ctx.stride)
+        gin, gx, gy = torch.ops.shiftgcn.tshift_bwd(grad_output, input, xpos.detach(),
+                                                    ypos.detach(), ctx.stride, True)
         return gin, gx, gy, None
 
 

@@ -12,18 +12,19 @@ reference's pybind extension (``model/Temporal_shift/cuda/shift_cuda.cpp:19-47``
 With ``sys.modules["shift_cuda"] = shiftgcn.shift_cuda`` the reference's unchanged
 ``cuda/shift.py`` runs its ``ShiftFunction`` on the gfx950 kernels.
 """
+import torch
+
 from . import ops
+from . import torch_ops  # noqa: F401  (registers torch.ops.shiftgcn.*)
 
 
 def forward(input, xpos, ypos, stride):  # noqa: A002 (reference names)
-    ops.check_input(input, "input")
-    return ops.tshift_fwd(input, xpos.contiguous(), ypos.contiguous(), stride,
-                          ypos_is_raw=False)
+    ops.check_input(input, "input", input.dtype)
+    return torch.ops.shiftgcn.tshift_fwd(input, xpos, ypos, stride, False)
 
 
 def backward(grad_output, input, output, xpos, ypos, stride):  # noqa: A002
-    ops.check_input(grad_output, "grad_output")
-    ops.check_input(output, "output")
-    gin, gx, gy = ops.tshift_bwd(grad_output, input.contiguous(), xpos.contiguous(),
-                                 ypos.contiguous(), stride, ypos_is_raw=False)
+    ops.check_input(grad_output, "grad_output", grad_output.dtype)
+    ops.check_input(output, "output", output.dtype)
+    gin, gx, gy = torch.ops.shiftgcn.tshift_bwd(grad_output, input, xpos, ypos, stride, False)
     return [gin, gx, gy]

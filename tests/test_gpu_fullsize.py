@@ -1,7 +1,7 @@
 """Full-size parity on the GPU (the BASELINE configs at their real sizes).
 
 The oracle (``oracle/model_oracle.py``, pinned to the reference's own modules by the golden
-fixtures) is run on the GPU with the torch-gather temporal shift of ``tests/torch_shift.py``
+fixtures) is run on the GPU with the torch-gather temporal shift of ``oracle/torch_shift.py``
 in place of ``shift_cuda`` (BASELINE config 1's "naive torch.gather fallback"), in fp32
 and in fp64, beside the HIP path:
 
@@ -23,7 +23,7 @@ import pytest
 import torch
 
 import formula
-import torch_shift as ts
+from oracle import torch_shift as ts
 from oracle import model_oracle as mo
 
 pytestmark = pytest.mark.gpu

@@ -139,9 +139,9 @@ def test_fma_contracted_variant_is_within_one_rounding(stride):
 
 @pytest.mark.parametrize("stride", [1, 2])
 def test_torch_restatement_matches_numpy_oracle(stride):
-    """tests/torch_shift.py (the on-device eager reference of the full-size parity tests)
+    """oracle/torch_shift.py (the on-device eager reference of the full-size parity tests)
     agrees with the numpy oracle on the CPU."""
-    import torch_shift as ts
+    from oracle import torch_shift as ts
     rng = np.random.default_rng(5 + stride)
     B, C, H, W = 2, 8, 30, 25
     x = rng.standard_normal((B, C, H, W)).astype(np.float32)
