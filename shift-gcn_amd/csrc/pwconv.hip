@@ -70,6 +70,21 @@ struct FwdArgs {
   int relu;
 };
 
+// Diagnostic builds only (tools/bench/pwbench -DSGCN_PW_STAMPS): per-workgroup cycle
+// stamps of the forward contraction's phases, written by one lane to a debug buffer that
+// nothing else reads. Compiled out of the product library.
+#ifdef SGCN_PW_STAMPS
+__device__ unsigned long long* g_pw_stamps;
+#define SGCN_PW_STAMP(i)                                                                  \
+  do {                                                                                    \
+    if (threadIdx.x == 0)                                                                 \
+      g_pw_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (i)] =              \
+          __builtin_amdgcn_s_memtime();                                                   \
+  } while (0)
+#else
+#define SGCN_PW_STAMP(i) do {} while (0)
+#endif
+
 __device__ __forceinline__ int pmod(int a, int V) {
   int r = a % V;
   return r < 0 ? r + V : r;
@@ -130,6 +145,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   __shared__ unsigned ycol_s[BN];   // per tile column: byte offset of (b, t) in Y
   __shared__ int v_s[BN];           // per tile column: joint v
 
+  SGCN_PW_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
@@ -228,6 +244,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   load_stage(0);
   store_stage(0, 0);
   __syncthreads();
+  SGCN_PW_STAMP(1);
   for (int s = 0; s < nstage; ++s) {
     const int cur = s & 1;
     if (s + 1 < nstage) {
@@ -265,6 +282,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
     __syncthreads();
   }
 
+  SGCN_PW_STAMP(2);
   // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5) ----
   const auto yr = make_rsrc(p.y.ptr, p.y_bytes);
   const unsigned ycs4 = (unsigned)(p.y.cstride * 4);
@@ -314,6 +332,10 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   };
   if (p.relu) epilogue(std::true_type{});
   else epilogue(std::false_type{});
+#ifdef SGCN_PW_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);   // stores issued and drained
+#endif
+  SGCN_PW_STAMP(3);
 }
 
 // ------------------------------------------------------------------------------------

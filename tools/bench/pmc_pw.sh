@@ -11,6 +11,6 @@ P3="SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_
 i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/p$i -o run -- $ROOT/tools/bench/pwbench "$@" > $OUT/p$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/p$i -o run -- $ROOT/tools/bench/${PWBIN:-pwbench} "$@" > $OUT/p$i.log 2>&1
 done
 echo PMC_DONE
