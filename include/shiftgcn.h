@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 11
+#define SGCN_ABI_VERSION 13
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -144,8 +144,40 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
                 int y_tstride, int y_rsign, int relu, int accumulate, int B, int M, int K,
                 int T, int V, void* stream);
 
+/* Shift_tcn's shift_in fused into its temporal_linear (shift_gcn.py:66-70):
+ *   Y[b][m][n] = act( sum_k w[m*K + k] * S_k(b, n) + bias[m] ),
+ *   S_k = shift_k(in_scale[k] * X[b][k] + in_shift[k])   (stride-1 temporal shift,
+ *   xpos/ypos per channel, shift_cuda_kernel.cu:11-76; in_scale/in_shift = Shift_tcn.bn's
+ *   apply coefficients, both NULL = identity).
+ * The shifted operand is formed from four taps of X while the contraction stages its
+ * tiles (same arithmetic as sgcn_tshift_fwd, so Y is bit-identical to sgcn_tshift_fwd +
+ * sgcn_pw_fwd); it is never read back from memory. x_shifted (optional, layout of x):
+ * also store S there from the same registers (the weight gradient's operand; NULL = not
+ * written, and sgcn_pw_dw_tshift re-forms it instead). w is (M, K) k-contiguous (Conv2d
+ * weight); relu != 0 applies ReLU. Workspace: sgcn_pw_tshift_ws_bytes(K) (the per-channel
+ * shift table). */
+size_t sgcn_pw_tshift_ws_bytes(int K);
+int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long long x_bstride,
+                       long long x_cstride, const float* xpos, const float* ypos,
+                       const float* in_scale, const float* in_shift, float* x_shifted,
+                       void* ws, size_t ws_bytes, float* y, long long y_bstride,
+                       long long y_cstride, int relu, int B, int M, int K, int T, int V,
+                       void* stream);
+
 /* Workspace bytes for sgcn_pw_dw. */
 size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V);
+
+/* Weight gradient of the fused Shift_tcn contraction (sgcn_pw_fwd_tshift): as sgcn_pw_dw
+ * with X'(b,c,n) = shift_c(in_scale[c] * X[b][c] + in_shift[c])(n) formed from four taps
+ * of X while staging (the shifted tensor is never read or written); G plain. Workspace:
+ * sgcn_pw_dw_tshift_ws_bytes (shift table + deterministic split-K slabs). */
+size_t sgcn_pw_dw_tshift_ws_bytes(int B, int M, int Nc, int T, int V);
+int sgcn_pw_dw_tshift(const float* g, long long g_bstride, long long g_cstride, const float* x,
+                      long long x_bstride, long long x_cstride, const float* xpos,
+                      const float* ypos, const float* in_scale, const float* in_shift,
+                      float* dw, int dw_transpose, int dw_accumulate, float* dbias,
+                      int dbias_accumulate, void* ws, size_t ws_bytes, int B, int M, int Nc,
+                      int T, int V, void* stream);
 
 /* Weight gradient over every position: dW[m][c] (+)= sum_{b,n} G(b,m,n) * X'(b,c,n)
  * (stored [c][m] when dw_transpose, e.g. Linear_weight's (C_in, C_out) layout) and

@@ -61,6 +61,8 @@ struct FwdArgs {
   const float* bias;
   Plane x;
   const float* mask;  // optional mask[v*K + k] multiplied into B (Shift_gcn feature mask)
+  const int* ts;      // TSH: per-channel temporal-shift table (tshift_params_kernel), K x 12
+  float* xs;          // TSH (optional): also store the shifted operand (layout of x)
   OutPlane y;
   int M, K, T, V;
   int B;
@@ -114,6 +116,55 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, unsign
 __device__ __forceinline__ int rot_step(int d, int rsign, int V) { return pmod(d * rsign, V); }
 
 // ------------------------------------------------------------------------------------
+// Temporal shift fused into a contraction operand (Shift_tcn: bn -> shift_in ->
+// temporal_linear, shift_gcn.py:66-69). The operand element (k, t, v) is
+//   shift_k(a_k * H[k] + b_k)[t, v]     (stride 1, shift_cuda_kernel.cu:11-76)
+// formed from four taps of H while the operand tile is staged, with exactly the
+// arithmetic of tshift.hip's AFFINE path (per-tap multiply then add, zero outside the
+// plane, the .cu:73 blend in order, no contraction), so it is bit-identical to writing
+// the shifted tensor with sgcn_tshift_fwd and contracting it. Per-channel geometry comes
+// from a table (12 words per channel, 48-byte rows for scalar loads):
+//   [0] off = y1*V + x1, [1] y1, [2] x1, [3] dx, [4] dy, [5] a, [6] b
+// ------------------------------------------------------------------------------------
+constexpr int kTsWords = 12;
+
+__device__ __forceinline__ float ts_tap(float q, float a, float b, bool ok) {
+#pragma clang fp contract(off)
+  const float v = q * a + b;
+  return ok ? v : 0.f;
+}
+
+__device__ __forceinline__ float ts_blend(float q11, float q21, float q12, float q22, float dx,
+                                          float dy) {
+#pragma clang fp contract(off)
+  const float omdx = 1.f - dx, omdy = 1.f - dy;
+  return q11 * omdx * omdy + q21 * dx * omdy + q12 * omdx * dy + q22 * dx * dy;
+}
+
+// per-channel table: x1 = floorf(x), dx = x - x1 (.cu:49-71), same for y (stride 1: no
+// +0.5, shift.py:17-18 applies to stride != 1 only)
+__global__ void tshift_params_kernel(const float* __restrict__ xpos,
+                                     const float* __restrict__ ypos,
+                                     const float* __restrict__ scale,
+                                     const float* __restrict__ shift, int K, int V,
+                                     int* __restrict__ tab) {
+#pragma clang fp contract(off)
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const float x = xpos[k], y = ypos[k];
+  const int x1 = (int)floorf(x), y1 = (int)floorf(y);
+  int* r = tab + k * kTsWords;
+  r[0] = y1 * V + x1;
+  r[1] = y1;
+  r[2] = x1;
+  r[3] = __float_as_int(x - (float)x1);
+  r[4] = __float_as_int(y - (float)y1);
+  r[5] = __float_as_int(scale ? scale[k] : 1.f);
+  r[6] = __float_as_int(shift ? shift[k] : 0.f);
+  for (int i = 7; i < kTsWords; ++i) r[i] = 0;
+}
+
+// ------------------------------------------------------------------------------------
 // forward / dX. Positions are flattened over (sample, t, v) so a tile may span samples;
 // one tile = all M (<= BM) x BN positions, so X crosses HBM once in long contiguous
 // runs per channel row; BK = 16 double-buffered LDS stages, one barrier per stage.
@@ -126,8 +177,10 @@ __device__ __forceinline__ int rot_step(int d, int rsign, int V) { return pmod(d
 // from per-element selects. Only the joint-shift rotation (XROT) and the feature mask
 // cost VALU per loaded element.
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM>
+template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM,
+          bool TSH = false>
 __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
+  static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = 16;
   constexpr int MI = BM / WM / 32;
@@ -156,6 +209,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   const auto xr = make_rsrc(p.x.ptr, p.x_bytes);
   const auto ar = make_rsrc(p.A, p.a_bytes);
   const auto mr = make_rsrc(MASK ? p.mask : p.A, MASK ? p.mask_bytes : 0u);
+  const auto xsr = make_rsrc(TSH && p.xs ? p.xs : p.A, TSH && p.xs ? p.x_bytes : 0u);
 
   for (int i = tid; i < BM; i += NT) {
     bias_s[i] = (p.bias && m0 + i < M) ? p.bias[m0 + i] : 0.f;
@@ -165,8 +219,9 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   // ---- B column of this thread (fixed for the tile) ----
   const int nb = tid % BN;
   const int kb0 = __builtin_amdgcn_readfirstlane(tid / BN);
-  int vv = 0;
+  int vv = 0, tt = 0;
   unsigned xcol = p.x_bytes;   // out of range: loads return 0
+  const bool colok = p0 + nb < P;
   {
     const int pc = p0 + nb;
     unsigned ycol = p.y_bytes;   // out of range: stores dropped
@@ -174,6 +229,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
       const int b = pc / N;
       const int n = pc - b * N;
       const int t = n / V;
+      tt = t;
       vv = n - t * V;
       xcol = (unsigned)(((long long)b * p.x.bstride + (long long)t * p.x.tstride * V +
                          (XROT ? 0 : vv)) * 4);
@@ -200,11 +256,32 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   const unsigned astep = AMC ? (unsigned)((NT / BM) * lda * 4) : (unsigned)((NT / BK) * lda * 4);
 
   float ra[A_PER], rb[B_PER], rm[MASK ? B_PER : 1];
+  float rq[TSH ? B_PER : 1][TSH ? 3 : 1];   // TSH: taps q21, q12, q22 (q11 in rb)
+  const unsigned v4 = (unsigned)(V * 4);
   auto load_stage = [&](int k0) {
     int cv = cv0;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
+      if (TSH) {
+        // four taps of H around (t + y1, v + x1); a tap outside the plane is masked in
+        // store_stage (its address is clamped / past the extent, never faulting)
+        // An in-plane tap lies inside [0, x_bytes - 4 - row offset], so clamping every
+        // tap offset into that range only moves taps that store_stage masks, and no
+        // address (voffset + soffset) ever leaves the operand; a column past P keeps the
+        // out-of-range marker for all four taps.
+        const int off = p.ts[row * kTsWords];
+        const unsigned so = (unsigned)row * xcs4;
+        const int vo = (int)xcol + off * 4, lim = (int)(p.x_bytes - 4u - so);
+        auto tap = [&](int d) {
+          return colok ? (unsigned)min(max(vo + d, 0), lim) : p.x_bytes;
+        };
+        rb[i] = bload(xr, tap(0), so);
+        rq[i][0] = bload(xr, tap(4), so);
+        rq[i][1] = bload(xr, tap((int)v4), so);
+        rq[i][2] = bload(xr, tap((int)v4 + 4), so);
+        continue;
+      }
       const unsigned voff = XROT ? xcol + (unsigned)(cv * 4) : xcol;
       rb[i] = bload(xr, voff, (unsigned)row * xcs4);
       if (MASK) rm[i] = bload(mr, mcol, (unsigned)row * 4u);
@@ -217,10 +294,27 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) ra[i] = bload(ar, avoff, ak0 + (unsigned)i * astep);
   };
+  const int T = p.T;
   auto store_stage = [&](int buf, int k0) {
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i)
-      Bs[buf][(kb0 + i * KSTEP_B) * BP + nb] = MASK ? rb[i] * rm[i] : rb[i];
+    for (int i = 0; i < B_PER; ++i) {
+      float val = MASK ? rb[i] * rm[i] : rb[i];
+      if (TSH) {
+        const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
+        const int* pr = p.ts + row * kTsWords;
+        const int tr = tt + pr[1], vr = vv + pr[2];
+        const float a = __int_as_float(pr[5]), b = __int_as_float(pr[6]);
+        const bool r0 = (unsigned)tr < (unsigned)T, r1 = (unsigned)(tr + 1) < (unsigned)T;
+        const bool c0 = (unsigned)vr < (unsigned)V, c1 = (unsigned)(vr + 1) < (unsigned)V;
+        val = ts_blend(ts_tap(rb[i], a, b, r0 && c0), ts_tap(rq[i][0], a, b, r0 && c1),
+                       ts_tap(rq[i][1], a, b, r1 && c0), ts_tap(rq[i][2], a, b, r1 && c1),
+                       __int_as_float(pr[3]), __int_as_float(pr[4]));
+        // side output: the shifted operand itself, for the weight gradient (each element
+        // is formed exactly once when one M-block covers all M)
+        if (p.xs) bstore(xsr, val, colok ? xcol : p.x_bytes, (unsigned)row * xcs4);
+      }
+      Bs[buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
+    }
     if (!AMC && k0 + BK > K) {   // k-contiguous A: a k past K aliases the next row
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) ra[i] = keep(ra[i], k0 + ak < K);
@@ -345,6 +439,7 @@ struct DwArgs {
   Plane g;            // A operand rows m: G(b, m, n)
   Plane x;            // B operand rows n: X(b, c, n)
   const float* mask;  // optional mask[v*Nc + c] on X
+  const int* ts;      // TSH: X is the temporal shift of a*X+b (table, Nc x kTsWords)
   float* slab;        // [S][M][Nc]
   float* bslab;       // optional [S][M] row sums of G
   int M, Nc, T, V, B;
@@ -512,8 +607,10 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
 // and RPW = 64/BKP rows per wave instruction; the row offset is a wave-uniform soffset.
 // Positions past the split's end load 0 through the descriptor range.
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int BKP, bool MASK, bool GROT, bool XROT, bool BIAS>
+template <int BM, int BN, int WM, int WN, int BKP, bool MASK, bool GROT, bool XROT, bool BIAS,
+          bool TSH = false>
 __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
+  static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
   constexpr int NT = 64 * WM * WN;
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
   // row pitch: the per-chunk stores put BKP positions x (32/BKP) rows in one 32-lane
@@ -528,6 +625,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
   static_assert(BM % RSTEP == 0 && BN % RSTEP == 0 && 64 % BKP == 0, "bad tile");
   __shared__ float As[2][BKP * AP];
   __shared__ float Bs[2][BKP * BP];
+  __shared__ int ts_s[TSH ? BN * 8 : 1];   // TSH: the tile's channel table (8 words/row)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -562,6 +660,16 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
   float ra[G_PER], rb[X_PER], rm[MASK ? X_PER : 1], rsum[BIAS ? G_PER : 1];
 #pragma unroll
   for (int i = 0; i < (BIAS ? G_PER : 1); ++i) rsum[i] = 0.f;
+  float rq[TSH ? X_PER : 1][TSH ? 3 : 1];   // TSH: taps q21, q12, q22 (q11 in rb)
+  int tl = 0, vl = 0;                        // TSH: (t, v) of the staged chunk
+  const int v4 = V * 4;
+  if (TSH) {
+    for (int i = tid; i < BN * 8; i += NT) {
+      const int c = min(c0 + i / 8, p.Nc - 1);
+      ts_s[i] = p.ts[c * kTsWords + (i & 7)];
+    }
+    __syncthreads();
+  }
 
   auto load_chunk = [&]() {
     const bool ok = pp < p_end;
@@ -584,14 +692,34 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
     int cx = v + x_rot0;
     cx = cx >= V ? cx - V : cx;
     const unsigned mcol = (unsigned)((v * p.Nc + rsub) * 4);
+    if (TSH) {
+      // four taps of X around (t + y1, v + x1) per row (see pwg_fwd_kernel); an in-plane
+      // tap never has a negative offset, so the clamps only move taps that are masked
+      // (tap offsets clamped into the row's extent; positions past the split keep the
+      // out-of-range marker: see pwg_fwd_kernel)
+      tl = t;
+      vl = v;
 #pragma unroll
-    for (int i = 0; i < X_PER; ++i) {
-      const unsigned voff = xb + lx + (unsigned)((XROT ? cx : v) * 4);
-      rb[i] = bload(xr, voff, (unsigned)(c0 + rw + i * RSTEP) * xcs4);
-      if (MASK) rm[i] = bload(mr, mcol, (unsigned)(c0 + rw + i * RSTEP) * 4u);
-      if (XROT) {
-        cx += x_step;
-        cx = cx >= V ? cx - V : cx;
+      for (int i = 0; i < X_PER; ++i) {
+        const int off = ts_s[(rw + rsub + i * RSTEP) * 8];
+        const unsigned so = (unsigned)(c0 + rw + i * RSTEP) * xcs4;
+        const int vo = (int)(xb + lx) + (v + off) * 4, lim = (int)(p.x_bytes - 4u - so);
+        auto tap = [&](int d) { return ok ? (unsigned)min(max(vo + d, 0), lim) : p.x_bytes; };
+        rb[i] = bload(xr, tap(0), so);
+        rq[i][0] = bload(xr, tap(4), so);
+        rq[i][1] = bload(xr, tap(v4), so);
+        rq[i][2] = bload(xr, tap(v4 + 4), so);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < X_PER; ++i) {
+        const unsigned voff = xb + lx + (unsigned)((XROT ? cx : v) * 4);
+        rb[i] = bload(xr, voff, (unsigned)(c0 + rw + i * RSTEP) * xcs4);
+        if (MASK) rm[i] = bload(mr, mcol, (unsigned)(c0 + rw + i * RSTEP) * 4u);
+        if (XROT) {
+          cx += x_step;
+          cx = cx >= V ? cx - V : cx;
+        }
       }
     }
     // advance this lane's position by one chunk
@@ -609,8 +737,20 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
       if (BIAS) rsum[i] += ra[i];
     }
 #pragma unroll
-    for (int i = 0; i < X_PER; ++i)
-      Bs[buf][kq * BP + rw + rsub + i * RSTEP] = MASK ? rb[i] * rm[i] : rb[i];
+    for (int i = 0; i < X_PER; ++i) {
+      float val = MASK ? rb[i] * rm[i] : rb[i];
+      if (TSH) {
+        const int* pr = ts_s + (rw + rsub + i * RSTEP) * 8;
+        const int tr = tl + pr[1], vr = vl + pr[2];
+        const float a = __int_as_float(pr[5]), bb = __int_as_float(pr[6]);
+        const bool r0 = (unsigned)tr < (unsigned)T, r1 = (unsigned)(tr + 1) < (unsigned)T;
+        const bool q0 = (unsigned)vr < (unsigned)V, q1 = (unsigned)(vr + 1) < (unsigned)V;
+        val = ts_blend(ts_tap(rb[i], a, bb, r0 && q0), ts_tap(rq[i][0], a, bb, r0 && q1),
+                       ts_tap(rq[i][1], a, bb, r1 && q0), ts_tap(rq[i][2], a, bb, r1 && q1),
+                       __int_as_float(pr[3]), __int_as_float(pr[4]));
+      }
+      Bs[buf][kq * BP + rw + rsub + i * RSTEP] = val;
+    }
   };
 
   f32x16 acc[MI][NJ];
@@ -733,6 +873,14 @@ void launch_pwg(const FwdArgs& a, bool accum, hipStream_t st) {
 #undef SGCN_PWG
 }
 
+template <int BM, int BN, int WM, int WN>
+void launch_pwg_tsh(const FwdArgs& a, hipStream_t st) {
+  const long long P = (long long)a.B * a.T * a.V;
+  dim3 grid((unsigned)((P + BN - 1) / BN), (a.M + BM - 1) / BM);
+  pwg_fwd_kernel<BM, BN, WM, WN, false, false, false, false, true>
+      <<<grid, 64 * WM * WN, 0, st>>>(a);
+}
+
 // byte extent of a plane operand: one past its last addressed element
 unsigned plane_bytes(long long bstride, long long cstride, int tstride, int B, int C, int T,
                      int V) {
@@ -768,6 +916,15 @@ void launch_dw3_t(const DwArgs& a, int S, int tiles, hipStream_t st) {
   dim3 grid(tiles, S);
   const bool mask = a.mask != nullptr, gr = a.g.rsign != 0, xr = a.x.rsign != 0,
              bias = a.bslab != nullptr;
+  if (a.ts) {   // temporal-shift X operand: plain G, no mask / rotation
+    if (bias)
+      pw_dw3_kernel<BM, BN, WM, WN, BKP, false, false, false, true, true>
+          <<<grid, 64 * WM * WN, 0, st>>>(a);
+    else
+      pw_dw3_kernel<BM, BN, WM, WN, BKP, false, false, false, false, true>
+          <<<grid, 64 * WM * WN, 0, st>>>(a);
+    return;
+  }
 #define SGCN_DW3(MS, GR, XR, BI) \
   pw_dw3_kernel<BM, BN, WM, WN, BKP, MS, GR, XR, BI><<<grid, 64 * WM * WN, 0, st>>>(a)
 #define SGCN_DW3_BI(MS, GR, XR) (bias ? SGCN_DW3(MS, GR, XR, true) : SGCN_DW3(MS, GR, XR, false))
@@ -848,7 +1005,7 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   SGCN_REQUIRE((long long)(B - 1) * y_bstride + (long long)M * y_cstride + (long long)T * y_tstride * V < (1LL << 29));
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(w && x && y);
-  FwdArgs a;
+  FwdArgs a{};   // value-initialised: every optional pointer (mask, ts) starts null
   a.A = w;
   a.lda = w_mcontig ? M : K;
   a.a_mcontig = w_mcontig;
@@ -875,11 +1032,109 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   return 0;
 }
 
+size_t sgcn_pw_tshift_ws_bytes(int K) { return (size_t)K * kTsWords * sizeof(int); }
+
+int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long long x_bstride,
+                       long long x_cstride, const float* xpos, const float* ypos,
+                       const float* in_scale, const float* in_shift, float* x_shifted,
+                       void* ws, size_t ws_bytes, float* y, long long y_bstride,
+                       long long y_cstride, int relu, int B, int M, int K, int T, int V,
+                       void* stream) {
+  SGCN_REQUIRE(B >= 0 && M > 0 && K > 0 && K <= 256 && T >= 0 && V > 0 && V < 32768);
+  SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
+  SGCN_REQUIRE(x_cstride * (long long)K < (1LL << 31) && y_cstride * (long long)M < (1LL << 31));
+  SGCN_REQUIRE(x_cstride >= (long long)T * V && y_cstride >= (long long)T * V);
+  SGCN_REQUIRE((long long)B * T * V < (1LL << 31));
+  SGCN_REQUIRE((long long)(B - 1) * x_bstride + (long long)K * x_cstride + (long long)T * V < (1LL << 29));
+  SGCN_REQUIRE((long long)(B - 1) * y_bstride + (long long)M * y_cstride + (long long)T * V < (1LL << 29));
+  if (B == 0 || T == 0) return 0;
+  SGCN_REQUIRE(w && x && y && xpos && ypos && ws && ws_bytes >= sgcn_pw_tshift_ws_bytes(K));
+  hipStream_t st = (hipStream_t)stream;
+  tshift_params_kernel<<<(K + 63) / 64, 64, 0, st>>>(xpos, ypos, in_scale, in_shift, K, V,
+                                                     (int*)ws);
+  SGCN_LAUNCH_CHECK();
+  FwdArgs a{};
+  a.A = w;
+  a.lda = K;
+  a.a_mcontig = 0;
+  a.bias = bias;
+  a.x = {x, x_bstride, x_cstride, 1, 0};
+  a.mask = nullptr;
+  a.ts = (const int*)ws;
+  a.xs = x_shifted;
+  a.y = {y, y_bstride, y_cstride, 1, 0};
+  a.M = M;
+  a.K = K;
+  a.T = T;
+  a.V = V;
+  a.B = B;
+  a.x_bytes = plane_bytes(x_bstride, x_cstride, 1, B, K, T, V);
+  a.y_bytes = plane_bytes(y_bstride, y_cstride, 1, B, M, T, V);
+  a.a_bytes = (unsigned)((long long)M * K * 4);
+  a.mask_bytes = 0u;
+  a.relu = relu ? 1 : 0;
+  if (M <= 64) launch_pwg_tsh<64, 256, 2, 4>(a, st);
+  else if (M <= 128) launch_pwg_tsh<128, 256, 2, 4>(a, st);
+  else launch_pwg_tsh<256, 128, 4, 2>(a, st);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
 size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V) {
   if (use_dw3(M, Nc)) return dw3_ws_bytes(B, M, Nc, T, V);
   const int tiles = ((M + dw_tile(M) - 1) / dw_tile(M)) * ((Nc + dw_tile(Nc) - 1) / dw_tile(Nc));
   const int S = dw_splits(M, Nc, B, T * V, tiles);
   return (size_t)S * ((size_t)M * Nc + M) * sizeof(float);
+}
+
+size_t sgcn_pw_dw_tshift_ws_bytes(int B, int M, int Nc, int T, int V) {
+  return sgcn_pw_tshift_ws_bytes(Nc) + dw3_ws_bytes(B, M, Nc, T, V);
+}
+
+int sgcn_pw_dw_tshift(const float* g, long long g_bstride, long long g_cstride, const float* x,
+                      long long x_bstride, long long x_cstride, const float* xpos,
+                      const float* ypos, const float* in_scale, const float* in_shift,
+                      float* dw, int dw_transpose, int dw_accumulate, float* dbias,
+                      int dbias_accumulate, void* ws, size_t ws_bytes, int B, int M, int Nc,
+                      int T, int V, void* stream) {
+  SGCN_REQUIRE(B > 0 && M > 0 && Nc > 0 && T > 0 && V > 0 && V < 32768);
+  SGCN_REQUIRE(g && x && dw && ws && xpos && ypos);
+  SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
+  SGCN_REQUIRE(ws_bytes >= sgcn_pw_dw_tshift_ws_bytes(B, M, Nc, T, V));
+  SGCN_REQUIRE(g_cstride * (long long)M < (1LL << 31) && x_cstride * (long long)Nc < (1LL << 31));
+  SGCN_REQUIRE(g_cstride >= (long long)T * V && x_cstride >= (long long)T * V);
+  SGCN_REQUIRE((long long)(B - 1) * g_bstride + (long long)M * g_cstride + (long long)T * V < (1LL << 29));
+  SGCN_REQUIRE((long long)(B - 1) * x_bstride + (long long)Nc * x_cstride + (long long)T * V < (1LL << 29));
+  hipStream_t st = (hipStream_t)stream;
+  int* tab = (int*)ws;
+  float* slab = (float*)((char*)ws + sgcn_pw_tshift_ws_bytes(Nc));
+  tshift_params_kernel<<<(Nc + 63) / 64, 64, 0, st>>>(xpos, ypos, in_scale, in_shift, Nc, V, tab);
+  SGCN_LAUNCH_CHECK();
+  DwArgs a{};
+  a.g = {g, g_bstride, g_cstride, 1, 0};
+  a.x = {x, x_bstride, x_cstride, 1, 0};
+  a.mask = nullptr;
+  a.ts = tab;
+  a.M = M;
+  a.Nc = Nc;
+  a.T = T;
+  a.V = V;
+  a.B = B;
+  a.g_bytes = plane_bytes(g_bstride, g_cstride, 1, B, M, T, V);
+  a.x_bytes = plane_bytes(x_bstride, x_cstride, 1, B, Nc, T, V);
+  a.mask_bytes = 0u;
+  const int S = launch_dw3(a, st, slab, dbias != nullptr);
+  SGCN_LAUNCH_CHECK();
+  const int MN = M * Nc;
+  slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(slab, S, MN, M, Nc, dw, dw_transpose,
+                                                    dw_accumulate);
+  SGCN_LAUNCH_CHECK();
+  if (dbias) {
+    slab_reduce_kernel<<<(M + 63) / 64, 256, 0, st>>>(slab + (size_t)S * M * Nc, S, M, M, 1,
+                                                     dbias, 0, dbias_accumulate);
+    SGCN_LAUNCH_CHECK();
+  }
+  return 0;
 }
 
 int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_tstride,
@@ -892,7 +1147,7 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
   SGCN_REQUIRE(!mask || V <= kMaskMaxV);
   SGCN_REQUIRE(ws_bytes >= sgcn_pw_dw_ws_bytes(B, M, Nc, T, V));
   SGCN_REQUIRE(g_cstride * (long long)M < (1LL << 31) && x_cstride * (long long)Nc < (1LL << 31));
-  DwArgs a;
+  DwArgs a{};   // value-initialised: every optional pointer (mask, ts) starts null
   a.g = {g, g_bstride, g_cstride, g_tstride, g_rsign};
   a.x = {x, x_bstride, x_cstride, x_tstride, x_rsign};
   a.mask = mask;

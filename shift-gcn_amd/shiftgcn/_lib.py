@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen: one HIP runtime per proces
 
 LIB_NAME = "libshiftgcn_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 11
+ABI_VERSION = 13
 EINVAL = -22
 
 _lib = None
@@ -42,7 +42,13 @@ SIGNATURES = {
                                  _P]),
     "sgcn_pw_fwd": (_I, [_P, _I, _P, _P, _L, _L, _I, _I, _P, _P, _L, _L, _I, _I, _I, _I, _I,
                          _I, _I, _I, _I, _P]),
+    "sgcn_pw_tshift_ws_bytes": (_Z, [_I]),
+    "sgcn_pw_fwd_tshift": (_I, [_P, _P, _P, _L, _L, _P, _P, _P, _P, _P, _P, _Z, _P, _L, _L, _I,
+                                _I, _I, _I, _I, _I, _P]),
     "sgcn_pw_dw_ws_bytes": (_Z, [_I, _I, _I, _I, _I]),
+    "sgcn_pw_dw_tshift_ws_bytes": (_Z, [_I, _I, _I, _I, _I]),
+    "sgcn_pw_dw_tshift": (_I, [_P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P, _I, _I, _P, _I, _P,
+                               _Z, _I, _I, _I, _I, _I, _P]),
     "sgcn_pw_dw": (_I, [_P, _L, _L, _I, _I, _P, _L, _L, _I, _I, _P, _P, _I, _I, _P, _I, _P, _Z,
                         _I, _I, _I, _I, _I, _P]),
     "sgcn_moments_ws_bytes": (_Z, [_I, _I, _I, _I]),

@@ -30,6 +30,7 @@ caching allocator, so a whole training step can be captured in a hipGraph.
 """
 from __future__ import annotations
 
+import os
 import threading
 
 import torch
@@ -177,15 +178,26 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
         ast = ops.bn_finalize(h_moments, B, C, T * V, mod.bn)
     else:
         ast = ops.bn_eval_coef(mod.bn, C)
+    R = _empty(B, Cout, T, V, like=src)
+    tl = mod.temporal_linear
+    As = None
     if pre is not None:   # inference: H = relu(BN1d(Z) + res) formed while staging
         As = ops.tshift_fwd_pre(pre[0], si.xpos.detach(), si.ypos.detach(), si.stride, pre[1],
                                 pre[2], pre[3], ast)
+        ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
+    elif TSHIFT_FUSION:
+        # shift_in (with Shift_tcn.bn's apply) formed in the contraction's operand staging,
+        # never read back. Mode 1 (default) also stores it from the same registers for the
+        # weight gradient; mode 2 stores nothing and the weight gradient re-forms it from H
+        # (less memory, more VALU in an MFMA-bound kernel: DESIGN.md §Temporal fusion)
+        if TSHIFT_FUSION == 1:
+            As = torch.empty_like(H)
+        ops.pw_fwd_tshift(tl.weight, tl.bias, PV(H), si.xpos.detach(), si.ypos.detach(), ast,
+                          PV(R), Cout, C, T, V, relu=True, x_shifted=As)
     else:
         As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride,
                             scale=ast.scale, shift=ast.shift)
-    R = _empty(B, Cout, T, V, like=src)
-    tl = mod.temporal_linear
-    ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
+        ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
     To = T // stride
     if tail is not None:
         # inference: bn2 (eval) + residual + ReLU (+ next gather) fused into shift_out
@@ -220,7 +232,11 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None):
     tl = mod.temporal_linear
     dWt = torch.empty_like(tl.weight)
     dbt = torch.empty_like(tl.bias)
-    ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
+    if s.As is None:   # fused forward: re-form the shifted operand from H while staging
+        ops.pw_dw_tshift(PV(dRp), PV(H), si.xpos.detach(), si.ypos.detach(), s.ast, dWt, Cout, C,
+                         T, V, dbias=dbt)
+    else:
+        ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
     g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
     dAs = _empty(B, C, T, V, like=H)
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
@@ -393,6 +409,13 @@ def unit_backward(unit, s: UnitSaved, dout):
 # ======================================================================================
 # autograd Functions (module forward -> Function.apply(module, input, *params))
 # ======================================================================================
+# Shift_tcn's shift_in fused into temporal_linear's operand staging. 1 (default): fused
+# forward that also stores the shifted operand for the weight gradient; 2: nothing stored,
+# the weight gradient re-forms it from H; 0: the round-1 two-launch form (shift launch +
+# contraction). A/B knob: SGCN_TSHIFT_FUSION=0|1|2.
+TSHIFT_FUSION = int(os.environ.get("SGCN_TSHIFT_FUSION", "1"))
+
+
 def trainable(module):
     return [(n, p) for n, p in module.named_parameters() if p.requires_grad]
 

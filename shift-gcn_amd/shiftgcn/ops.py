@@ -358,6 +358,71 @@ def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=Fals
     return dw
 
 
+def pw_fwd_tshift(w, bias, x: PlaneView, xpos, ypos, st, out: PlaneView, M, K, T, V,
+                  relu=False, x_shifted=None):
+    """Shift_tcn's shift_in fused into temporal_linear (sgcn_pw_fwd_tshift):
+    out = act(w @ shift(st.scale*x + st.shift) + bias); the shifted operand is formed while
+    staging and never read back (``x_shifted``: optionally stored, layout of x, for the
+    weight gradient). ``st``: the BnStats of Shift_tcn.bn (None = identity); w is (M, K)
+    k-contiguous."""
+    check_input(w, "weight")
+    _opt(bias, "bias")
+    if x.tstride != 1 or x.rsign != 0 or out.tstride != 1 or out.rsign != 0:
+        raise ValueError("pw_fwd_tshift: plain planes only")
+    B = x.t.shape[0]
+    lib = _lib.load()
+    P = B * T * V
+    nbytes = lib.sgcn_pw_tshift_ws_bytes(K)
+    ws = torch.empty((nbytes + 3) // 4, device=x.t.device, dtype=_F32)
+    bc = _batch_chunk([(x, K), (out, M)], B, T, V)
+    sc = st.scale if st is not None else None
+    sh = st.shift if st is not None else None
+    if x_shifted is not None:
+        check_input(x_shifted, "x_shifted")
+        if x_shifted.shape != x.t.shape or x_shifted.stride() != x.t.stride():
+            raise ValueError("x_shifted must have the layout of x")
+    nbx = 4.0 * P * (M + K * (2 if x_shifted is not None else 1))
+    with _timed("pw_fwd", 2.0 * P * M * K, nbx, x.t):
+        for b0 in range(0, B, bc):
+            nb = min(bc, B - b0)
+            xs = None if x_shifted is None else x_shifted.data_ptr() + 4 * b0 * x.bstride
+            rc = lib.sgcn_pw_fwd_tshift(_ptr(w), _ptr(bias), x.t.data_ptr() + 4 * b0 * x.bstride,
+                                        x.bstride, x.cstride, _ptr(xpos), _ptr(ypos), _ptr(sc),
+                                        _ptr(sh), xs, _ptr(ws), nbytes,
+                                        out.t.data_ptr() + 4 * b0 * out.bstride, out.bstride,
+                                        out.cstride, int(relu), nb, M, K, T, V, _stream(x.t))
+            _lib.check(rc, "sgcn_pw_fwd_tshift")
+    return out.t
+
+
+def pw_dw_tshift(g: PlaneView, x: PlaneView, xpos, ypos, st, dw, M, Nc, T, V, dbias=None):
+    """Weight/bias gradient of :func:`pw_fwd_tshift`: dW[m][c] = sum G * shift_c(a*x + b)
+    (sgcn_pw_dw_tshift, the shifted operand re-formed from x while staging)."""
+    check_input(dw, "dw")
+    _opt(dbias, "dbias")
+    if x.tstride != 1 or x.rsign != 0 or g.tstride != 1 or g.rsign != 0:
+        raise ValueError("pw_dw_tshift: plain planes only")
+    B = g.t.shape[0]
+    lib = _lib.load()
+    bc = _batch_chunk([(g, M), (x, Nc)], B, T, V)
+    nbytes = lib.sgcn_pw_dw_tshift_ws_bytes(bc, M, Nc, T, V)
+    ws = torch.empty((nbytes + 3) // 4, device=g.t.device, dtype=_F32)
+    P = B * T * V
+    sc = st.scale if st is not None else None
+    sh = st.shift if st is not None else None
+    with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t):
+        for b0 in range(0, B, bc):
+            nb = min(bc, B - b0)
+            first = b0 == 0
+            rc = lib.sgcn_pw_dw_tshift(g.t.data_ptr() + 4 * b0 * g.bstride, g.bstride, g.cstride,
+                                       x.t.data_ptr() + 4 * b0 * x.bstride, x.bstride, x.cstride,
+                                       _ptr(xpos), _ptr(ypos), _ptr(sc), _ptr(sh), _ptr(dw), 0,
+                                       int(not first), _ptr(dbias), int(not first), _ptr(ws),
+                                       nbytes, nb, M, Nc, T, V, _stream(g.t))
+            _lib.check(rc, "sgcn_pw_dw_tshift")
+    return dw
+
+
 # --------------------------------------------------------------------------------------
 # BatchNorm / unit tails
 # --------------------------------------------------------------------------------------

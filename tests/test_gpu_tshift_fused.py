@@ -1,0 +1,142 @@
+"""Shift_tcn's shift_in fused into its temporal_linear (north_star: "the learnable
+fractional temporal shift ... fused with its trailing pointwise 1x1 conv"; reference
+model/shift_gcn.py:66-69, shift_cuda_kernel.cu:11-76).
+
+* forward: ``sgcn_pw_fwd_tshift`` == ``sgcn_tshift_fwd`` (bn affine on the taps) followed
+  by ``sgcn_pw_fwd``, bit for bit (same tap arithmetic, same K order), including planes
+  whose position count is not a tile multiple, |ypos| > 1, x shifts of a whole joint, V=33;
+* weight gradient: ``sgcn_pw_dw_tshift`` == ``sgcn_pw_dw`` on the materialised shifted
+  tensor (bit for bit where both use the same split-K kernel, else within 1e-6 relative);
+* the side output (mode 1, default) is the shifted operand, element for element;
+* every fusion mode (0: two launches, 1: fused + side output, 2: the weight gradient re-forms
+  the operand) gives the same unit parity vs the oracle;
+* in a training step there is no separate shift_in launch: the only temporal-shift forward
+  launches left are the 10 shift_outs (whose output feeds bn2's statistics).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+CASES = [
+    # (B, K, M, T, V)
+    (3, 64, 64, 20, 25),
+    (2, 128, 128, 17, 25),      # P not a multiple of the 256-position tile
+    (2, 256, 256, 9, 25),
+    (3, 64, 64, 11, 33),
+    (1, 128, 256, 7, 25),
+]
+
+
+def _inputs(B, K, M, T, V, seed):
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(B, K, T, V, generator=g).to(DEV)
+    w = (torch.randn(M, K, generator=g) / K ** 0.5).to(DEV)
+    bias = torch.randn(M, generator=g).to(DEV)
+    xpos = ((torch.rand(K, generator=g) - 0.5) * 2e-8)
+    ypos = (torch.rand(K, generator=g) - 0.5) * 6          # |y| up to 3 (> 1 tap row)
+    xpos[0], ypos[0] = 1.0, 0.0                            # a whole-joint x shift
+    xpos[1] = -1.5
+    ypos[2] = float(T + 1)                                 # shifted out of the plane
+    scale = (torch.rand(K, generator=g) + 0.5).to(DEV)
+    shift = torch.randn(K, generator=g).to(DEV)
+    return h, w, bias, xpos.to(DEV), ypos.to(DEV), scale, shift
+
+
+class _St:
+    def __init__(self, scale, shift):
+        self.scale, self.shift = scale, shift
+
+
+@pytest.mark.parametrize("case", CASES, ids=["x".join(map(str, c)) for c in CASES])
+def test_fused_forward_bit_identical_to_two_launch(case):
+    from shiftgcn import ops
+    from shiftgcn.ops import PlaneView as PV
+    B, K, M, T, V = case
+    h, w, bias, xpos, ypos, scale, shift = _inputs(*case, seed=sum(case))
+    As = ops.tshift_fwd(h, xpos, ypos, 1, scale=scale, shift=shift)
+    r1 = torch.empty(B, M, T, V, device=DEV)
+    ops.pw_fwd(w, False, bias, PV(As), PV(r1), M, K, T, V, relu=True)
+    r2 = torch.empty(B, M, T, V, device=DEV)
+    ops.pw_fwd_tshift(w, bias, PV(h), xpos, ypos, _St(scale, shift), PV(r2), M, K, T, V,
+                      relu=True)
+    r3 = torch.empty(B, M, T, V, device=DEV)
+    xs = torch.full_like(h, float("nan"))
+    ops.pw_fwd_tshift(w, bias, PV(h), xpos, ypos, _St(scale, shift), PV(r3), M, K, T, V,
+                      relu=True, x_shifted=xs)
+    torch.cuda.synchronize()
+    assert torch.equal(r1, r2) and torch.equal(r1, r3)
+    assert torch.equal(xs, As)        # the side output is the shifted operand, every element
+
+
+@pytest.mark.parametrize("case", CASES, ids=["x".join(map(str, c)) for c in CASES])
+def test_fused_weight_gradient_matches_materialised(case):
+    from shiftgcn import ops
+    from shiftgcn.ops import PlaneView as PV
+    B, K, M, T, V = case
+    h, w, bias, xpos, ypos, scale, shift = _inputs(*case, seed=3 * sum(case))
+    gr = torch.randn(B, M, T, V, device=DEV)
+    As = ops.tshift_fwd(h, xpos, ypos, 1, scale=scale, shift=shift)
+    dw1 = torch.empty(M, K, device=DEV)
+    db1 = torch.empty(M, device=DEV)
+    ops.pw_dw(PV(gr), PV(As), dw1, M, K, T, V, dbias=db1)
+    dw2 = torch.empty(M, K, device=DEV)
+    db2 = torch.empty(M, device=DEV)
+    ops.pw_dw_tshift(PV(gr), PV(h), xpos, ypos, _St(scale, shift), dw2, M, K, T, V, dbias=db2)
+    # fp64 reference of the same contraction on the materialised operand
+    ref = torch.einsum("bmn,bkn->mk", gr.double().flatten(2), As.double().flatten(2))
+    torch.cuda.synchronize()
+    assert float((dw2.double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+    assert float((dw2 - dw1).abs().max()) <= 1e-6 * float(dw1.abs().max()) + 1e-7
+    assert float((db2 - db1).abs().max()) <= 1e-6 * float(db1.abs().max()) + 1e-7
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_unit_matches_oracle_in_every_fusion_mode(monkeypatch, mode):
+    """SGCN_TSHIFT_FUSION 0 (two launches) and 2 (weight gradient re-forms the operand)
+    give the same unit parity as the default mode 1 (tested by test_gpu_blocks)."""
+    import formula
+    import shiftgcn
+    from oracle import model_oracle as mo
+    from shiftgcn import fused
+    from test_gpu_blocks import _compare
+    monkeypatch.setattr(fused, "TSHIFT_FUSION", mode)
+    ref = mo.TCN_GCN_unit(64, 128, None, stride=2, num_point=25)
+    formula.fill_state(ref, seed=mode + 17)
+    ours = shiftgcn.TCN_GCN_unit(64, 128, None, stride=2, num_point=25).to(DEV)
+    ours.load_state_dict(ref.state_dict())
+    ref.train()
+    ours.train()
+    x = formula.tensor((3, 64, 18, 25), 50 + mode, 1.0)
+    g = formula.tensor((3, 128, 9, 25), 60 + mode, 1.0)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(g)
+    xo = x.to(DEV).requires_grad_(True)
+    yo = ours(xo)
+    yo.backward(g.to(DEV))
+    torch.cuda.synchronize()
+    _compare(ref, ours, xr, yr, xo, yo, f"mode{mode}")
+
+
+def test_training_step_has_no_shift_in_launch(monkeypatch):
+    import formula
+    import shiftgcn
+    from shiftgcn import fused, ops
+    assert fused.TSHIFT_FUSION
+    calls = {"affine": 0, "plain": 0}
+    real = ops.tshift_fwd
+
+    def spy(inp, xpos, ypos, stride, scale=None, **kw):
+        calls["affine" if scale is not None else "plain"] += 1
+        return real(inp, xpos, ypos, stride, scale=scale, **kw)
+
+    monkeypatch.setattr(ops, "tshift_fwd", spy)
+    m = shiftgcn.Model(num_class=60, num_point=25, num_person=2,
+                       graph="graph.ntu_rgb_d.Graph").to(DEV).train()
+    x = formula.tensor((2, 3, 16, 25, 2), 5, 1.0).to(DEV)
+    m(x).sum().backward()
+    torch.cuda.synchronize()
+    assert calls == {"affine": 0, "plain": 10}, calls
