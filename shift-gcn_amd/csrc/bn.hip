@@ -106,11 +106,21 @@ __device__ __forceinline__ bool feature_sums(const float2* __restrict__ part, in
   f = blockIdx.x * kFeat + fl;
   const int fc = min(f, F - 1);
   double ax = 0.0, ay = 0.0, axx = 0.0;
-  for (int b = q; b < B; b += kSlices) {
-    const float2 p = part[(size_t)b * F + fc];
-    ax += p.x;
-    ay += p.y;
-    axx += (double)p.x * p.x;
+  // 8 independent loads in flight per trip (a dependent load per partial left these
+  // latency-bound at ~8 us per launch); the summation order (b ascending) is unchanged
+  for (int b0 = q; b0 < B; b0 += kSlices * 8) {
+    float2 pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + u * kSlices;
+      pv[u] = b < B ? part[(size_t)b * F + fc] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ax += pv[u].x;
+      ay += pv[u].y;
+      axx += (double)pv[u].x * pv[u].x;
+    }
   }
   lx[q][fl] = ax;
   ly[q][fl] = ay;
@@ -582,7 +592,16 @@ __global__ __launch_bounds__(kFeat * kSlices) void mask_grad_finalize_kernel(
   const int f = blockIdx.x * kFeat + fl;
   const int fc = min(f, F - 1);
   double a = 0.0;
-  for (int b = q; b < B; b += kSlices) a += part[(size_t)b * F + fc];
+  for (int b0 = q; b0 < B; b0 += kSlices * 8) {
+    float pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + u * kSlices;
+      pv[u] = b < B ? part[(size_t)b * F + fc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += pv[u];
+  }
   ls[q][fl] = a;
   __syncthreads();
   if (q != 0 || f >= F) return;

@@ -718,10 +718,18 @@ __global__ __launch_bounds__(256) void tshift_pos_finalize_kernel(
   const int c = blockIdx.x * 32 + cl;
   const int cc = min(c, C - 1);
   double ax = 0.0, ay = 0.0;
-  for (int b = q; b < B; b += 8) {
-    const float2 p = pgrad[(size_t)b * C + cc];
-    ax += (double)p.x;
-    ay += (double)p.y;
+  for (int b0 = q; b0 < B; b0 += 64) {   // 8 independent loads in flight, same order
+    float2 pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + u * 8;
+      pv[u] = b < B ? pgrad[(size_t)b * C + cc] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ax += (double)pv[u].x;
+      ay += (double)pv[u].y;
+    }
   }
   lx[q][cl] = ax;
   ly[q][cl] = ay;

@@ -185,7 +185,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
         As = ops.tshift_fwd_pre(pre[0], si.xpos.detach(), si.ypos.detach(), si.stride, pre[1],
                                 pre[2], pre[3], ast)
         ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
-    elif TSHIFT_FUSION:
+    elif TSHIFT_FUSION and C >= TSHIFT_FUSION_MIN_C:
         # shift_in (with Shift_tcn.bn's apply) formed in the contraction's operand staging,
         # never read back. Mode 1 (default) also stores it from the same registers for the
         # weight gradient; mode 2 stores nothing and the weight gradient re-forms it from H
@@ -414,6 +414,8 @@ def unit_backward(unit, s: UnitSaved, dout):
 # the weight gradient re-forms it from H; 0: the round-1 two-launch form (shift launch +
 # contraction). A/B knob: SGCN_TSHIFT_FUSION=0|1|2.
 TSHIFT_FUSION = int(os.environ.get("SGCN_TSHIFT_FUSION", "1"))
+# fuse only from this many channels up (below, the two-launch form is used)
+TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "128"))
 
 
 def trainable(module):
