@@ -73,6 +73,11 @@ def parse():
                     help="--config ens: replay the ensemble forward as one hipGraph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--roofline", type=int, default=1)
+    ap.add_argument("--data", default=None,
+                    help="on-disk (N,3,T,V,M) float32 .npy clips (feeders/feeder.py format), "
+                         "memory-mapped and streamed to the GPU by shiftgcn.feeder; default: "
+                         "one synthetic batch resident in HBM")
+    ap.add_argument("--labels", default=None, help="(sample_name, label) pickle for --data")
     return ap.parse_args()
 
 
@@ -206,8 +211,33 @@ def main():
     gen = torch.Generator().manual_seed(1000 + rank)
     x = torch.randn(args.batch, 3, T, V, M, generator=gen).to(dev)
     label = torch.randint(0, num_class, (args.batch,), generator=gen).to(dev)
+    batches = None
+    if args.data:
+        # real clips: mmap -> pinned staging -> H2D on a copy stream, one batch ahead of
+        # the step (shiftgcn.feeder.DeviceBatchLoader); epochs repeat as needed
+        from shiftgcn.feeder import DeviceBatchLoader, Feeder
+        if not args.labels:
+            raise SystemExit("--data needs --labels")
+        if args.graph:
+            raise SystemExit("--data feeds a new batch every step: run it without --graph")
+        feeder = Feeder(args.data, args.labels)
+        if tuple(feeder.data.shape[1:]) != (3, T, V, M):
+            raise SystemExit(f"--data clips are {feeder.data.shape[1:]}, config "
+                             f"{args.config} needs (3, {T}, {V}, {M})")
+        loader = DeviceBatchLoader(feeder, args.batch, shuffle=True, drop_last=True,
+                                   device=dev, rank=rank, world_size=world)
+        if len(loader) == 0:
+            raise SystemExit("--data holds fewer clips than one global batch")
+
+        def _stream():
+            while True:
+                yield from loader
+        batches = _stream()
 
     def step():
+        if batches is not None:
+            xb, yb, _ = next(batches)
+            return train.train_step(model, opt, xb, yb, grad_sync=sync)
         return train.train_step(model, opt, x, label, grad_sync=sync)
 
     for _ in range(args.warmup):
@@ -321,7 +351,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic N(0,1) clips, random-init weights (seeded)",
+            "data": (f"on-disk clips {os.path.basename(args.data)} (mmap, streamed to HBM "
+                     "inside the timed region), random-init weights (seeded)" if args.data else
+                     "synthetic N(0,1) clips, random-init weights (seeded)"),
             "config": {"workload": f"{args.config.upper()} Shift-GCN training step "
                                    f"(fwd+CE+bwd+SGD), x=({args.batch},3,{T},{V},{M}) per GPU",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,

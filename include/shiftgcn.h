@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 13
+#define SGCN_ABI_VERSION 14
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -301,6 +301,46 @@ int sgcn_modalities(const float* joint, const int* parent, float* out_joint, flo
                     float* out_joint_motion, float* out_bone_motion, const float* scale,
                     const float* shift, int planes, int N, int C, int T, int V, int M,
                     void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Model head / tail of the training step (shift_gcn.py:193-216)
+ * ------------------------------------------------------------------------------------
+ * Model.forward's input side is x.permute(0,4,3,1,2).view(N, M*V*C, T) -> data_bn =
+ * BatchNorm1d(M*V*C) -> permute back to planes (N*M, C, T, V) (:194-198); features here
+ * are in the reference order f = m*V*C + v*C + c (pass perm_V = 0 to the finalizes).
+ * x is the (N, C, T, V, M) clip. */
+
+/* Bytes of the [N][M*V*C] float2 partials of sgcn_head_moments / sgcn_head_bwd_reduce. */
+size_t sgcn_head_ws_bytes(int N, int C, int V, int M);
+
+/* part[n][f] = {mean, M2} of x over t (data_bn training statistics; merge with
+ * sgcn_bn_finalize(part, N, M*V*C, T, 0, ...)). */
+int sgcn_head_moments(const float* x, float* part, int N, int C, int T, int V, int M,
+                      void* stream);
+
+/* y[(n*M + m), c, t, v] = x[n, c, t, v, m] * scale[f] + shift[f]: the permute and data_bn
+ * apply in one pass (scale/shift from sgcn_bn_finalize or sgcn_bn_eval_coef). */
+int sgcn_head_apply(const float* x, const float* scale, const float* shift, float* y, int N,
+                    int C, int T, int V, int M, void* stream);
+
+/* part[n][f] = {sum_t g, sum_t g*(x - mean[f])*invstd[f]}, g = the plane-layout gradient of
+ * y (feed sgcn_bn_bwd_finalize(part, N, M*V*C, N*T, 0, ...) for dgamma/dbeta/coef). */
+int sgcn_head_bwd_reduce(const float* g, const float* x, const float* mean, const float* invstd,
+                         float* part, int N, int C, int T, int V, int M, void* stream);
+
+/* dx[n, c, t, v, m] = k1[f]*g + k2[f]*x + k3[f], coef = [3][M*V*C] from
+ * sgcn_bn_bwd_finalize (only needed when the clip itself requires a gradient). */
+int sgcn_head_bwd_apply(const float* g, const float* x, const float* coef, float* dx, int N,
+                        int C, int T, int V, int M, void* stream);
+
+/* out[n][c] = x.view(N, M, C, P).mean(3).mean(1) (shift_gcn.py:211-214), x the last unit's
+ * (N*M, C, T', V) output, P = T'*V. */
+int sgcn_pool(const float* x, float* out, int N, int M, int C, long long P, void* stream);
+
+/* dx[n*M + m][c][p] = (dout[n][c] * (1/M)) * (1/P) (fp32 reciprocals): the pooling's
+ * backward, rounded exactly as autograd's mean backward on the device. */
+int sgcn_pool_bwd(const float* dout, float* dx, int N, int M, int C, long long P,
+                  void* stream);
 
 #ifdef __cplusplus
 }  /* extern "C" */

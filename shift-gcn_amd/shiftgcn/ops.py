@@ -455,6 +455,9 @@ def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
     st = BnStats(F, part.device)
     lib = _lib.load()
     track = training and bn.track_running_stats and bn.running_mean is not None
+    if track and bn.momentum is None:
+        # the cumulative moving average (momentum=None) is never used by the reference
+        raise NotImplementedError("BatchNorm momentum=None is not supported on the HIP path")
     momentum = bn.momentum if bn.momentum is not None else 0.0
     with _timed("finalize", 0, 4 * part.numel(), part):
         rc = lib.sgcn_bn_finalize(
@@ -596,3 +599,72 @@ def mask_grad_finalize(part, mask, B, C, V):
                                                  0, _stream(mask))
     _lib.check(rc, "sgcn_mask_grad_finalize")
     return dmask
+
+
+# --------------------------------------------------------------------------------------
+# model head (permute + data_bn) and tail (global average pool), shift_gcn.py:193-216
+# --------------------------------------------------------------------------------------
+def head_moments(x):
+    """{mean, M2} over t per (n, data_bn feature) of the (N, C, T, V, M) clip."""
+    check_input(x, "input")
+    N, C, T, V, M = x.shape
+    part = torch.empty((N * M * V * C * 2,), device=x.device, dtype=_F32)
+    with _timed("head", 0, 4 * x.numel(), x):
+        rc = _lib.load().sgcn_head_moments(_ptr(x), _ptr(part), N, C, T, V, M, _stream(x))
+    _lib.check(rc, "sgcn_head_moments")
+    return part
+
+
+def head_apply(x, st: BnStats):
+    """Planes (N*M, C, T, V) = data_bn(permuted clip) with the coefficients of ``st``."""
+    N, C, T, V, M = x.shape
+    y = torch.empty((N * M, C, T, V), device=x.device, dtype=_F32)
+    with _timed("head", 0, 8 * x.numel(), x):
+        rc = _lib.load().sgcn_head_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift), _ptr(y), N, C,
+                                         T, V, M, _stream(x))
+    _lib.check(rc, "sgcn_head_apply")
+    return y
+
+
+def head_bwd_reduce(g, x, st: BnStats):
+    check_input(g, "grad_output")
+    N, C, T, V, M = x.shape
+    part = torch.empty((N * M * V * C * 2,), device=x.device, dtype=_F32)
+    with _timed("head", 0, 8 * x.numel(), x):
+        rc = _lib.load().sgcn_head_bwd_reduce(_ptr(g), _ptr(x), _ptr(st.mean), _ptr(st.invstd),
+                                              _ptr(part), N, C, T, V, M, _stream(x))
+    _lib.check(rc, "sgcn_head_bwd_reduce")
+    return part
+
+
+def head_bwd_apply(g, x, coef):
+    N, C, T, V, M = x.shape
+    dx = torch.empty_like(x)
+    with _timed("head", 0, 12 * x.numel(), x):
+        rc = _lib.load().sgcn_head_bwd_apply(_ptr(g), _ptr(x), _ptr(coef), _ptr(dx), N, C, T, V,
+                                             M, _stream(x))
+    _lib.check(rc, "sgcn_head_bwd_apply")
+    return dx
+
+
+def pool(x, N, M):
+    """(N*M, C, T, V) -> (N, C): x.view(N, M, C, -1).mean(3).mean(1)."""
+    check_input(x, "input")
+    C = x.shape[1]
+    P = x.numel() // max(1, N * M * C)
+    out = torch.empty((N, C), device=x.device, dtype=_F32)
+    with _timed("pool", 0, 4 * x.numel(), x):
+        rc = _lib.load().sgcn_pool(_ptr(x), _ptr(out), N, M, C, P, _stream(x))
+    _lib.check(rc, "sgcn_pool")
+    return out
+
+
+def pool_bwd(dout, shape, N, M):
+    check_input(dout, "grad_output")
+    dx = torch.empty(shape, device=dout.device, dtype=_F32)
+    C = shape[1]
+    P = dx.numel() // max(1, N * M * C)
+    with _timed("pool", 0, 4 * dx.numel(), dout):
+        rc = _lib.load().sgcn_pool_bwd(_ptr(dout), _ptr(dx), N, M, C, P, _stream(dout))
+    _lib.check(rc, "sgcn_pool_bwd")
+    return dx

@@ -7,9 +7,10 @@ as the reference (``shift_gcn.py:14-216``), so reference checkpoints load unchan
 HIP recipes of :mod:`shiftgcn.fused`; there is no CPU path (CPU tensors raise like the
 reference's ``CHECK_INPUT``).
 
-Outside the hot path (SURVEY §8f "next"): ``Model``'s input permute + ``data_bn`` and the
-pooling + ``fc`` head use torch ops on the device; ``tcn`` with kernel_size != 1 (never
-instantiated by ``Model``) uses ``torch.nn.functional.conv2d`` on the device.
+``Model``'s input permute + ``data_bn`` and the global average pool run the HIP kernels of
+:mod:`shiftgcn.head`; the classifier ``fc`` is ``nn.Linear`` (a library
+GEMM on the device). ``tcn`` with kernel_size != 1 (never instantiated by ``Model``) uses
+``torch.nn.functional.conv2d`` on the device.
 """
 from __future__ import annotations
 
@@ -21,7 +22,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import fused
+from . import fused, head
 from .shift import Shift
 
 
@@ -192,9 +193,9 @@ class Model(nn.Module):
 
     def forward(self, x):
         N, C, T, V, M = x.size()
-        x = x.permute(0, 4, 3, 1, 2).contiguous().view(N, M * V * C, T)
-        x = self.data_bn(x)
-        x = x.view(N, M, V, C, T).permute(0, 1, 3, 4, 2).contiguous().view(N * M, C, T, V)
+        # permute -> data_bn -> permute back (:194-198) as one statistics pass + one
+        # fused apply pass over the clip
+        x = head.data_bn_planes(self.data_bn, x.contiguous())
         return self.forward_planes(x, N, M)
 
     def forward_planes(self, x, N, M):
@@ -204,9 +205,7 @@ class Model(nn.Module):
         with linked_units(units):
             for u in units:
                 x = u(x)
-        c_new = x.size(1)
-        x = x.view(N, M, c_new, -1)
-        x = x.mean(3).mean(1)
+        x = head.pool(x, N, M)        # x.view(N, M, C, -1).mean(3).mean(1)  (:211-214)
         return self.fc(x)
 
 
