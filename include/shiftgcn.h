@@ -338,7 +338,8 @@ int sgcn_head_bwd_apply(const float* g, const float* x, const float* coef, float
 int sgcn_pool(const float* x, float* out, int N, int M, int C, long long P, void* stream);
 
 /* dx[n*M + m][c][p] = (dout[n][c] * (1/M)) * (1/P) (fp32 reciprocals): the pooling's
- * backward, rounded exactly as autograd's mean backward on the device. */
+ * backward, rounded exactly as autograd's mean backward on the device. dx must be
+ * 16-byte aligned. */
 int sgcn_pool_bwd(const float* dout, float* dx, int N, int M, int C, long long P,
                   void* stream);
 

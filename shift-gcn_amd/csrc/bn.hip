@@ -96,9 +96,11 @@ __device__ __forceinline__ int ref_feature(int f, int perm_V, int F) {
 }
 
 // Per-feature sums over the batch of float2 partials, parallel over b: block = 32
-// features x 8 batch slices; the 8 slice sums are added in fixed order (deterministic).
-// Returns the three double sums (x, y, x*x) in the q == 0 threads.
-constexpr int kFeat = 32, kSlices = 8;
+// features x 32 batch slices; the 32 slice sums are added in fixed order (deterministic).
+// Returns the three double sums (x, y, x*x) in the q == 0 threads. These kernels are
+// latency-bound (a few MB of partials), so every partial of a thread is loaded in ONE
+// round trip for B <= 256 (8 loads in flight per thread).
+constexpr int kFeat = 32, kSlices = 32;
 __device__ __forceinline__ bool feature_sums(const float2* __restrict__ part, int B, int F,
                                              double& sx, double& sy, double& sxx, int& f) {
   __shared__ double lx[kSlices][kFeat], ly[kSlices][kFeat], lxx[kSlices][kFeat];

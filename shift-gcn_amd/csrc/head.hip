@@ -188,18 +188,30 @@ __global__ __launch_bounds__(kHT) void pool_kernel(const float* __restrict__ x,
 }
 
 // dx[n*M + m][c][p] = dout[n][c] / M / P (mean(1) then mean(3) backward, same order and
-// rounding as autograd). One thread per element; bytes: 4 per element (the dout read is cached).
+// rounding as autograd). Four consecutive elements per thread, one 16-byte store (the
+// tensor base is 16-byte aligned; rows of P elements may start mid-vector, so each lane
+// of the vector finds its own row). Bytes: 4 per element (the dout read is cached).
 __global__ __launch_bounds__(kHT) void pool_bwd_kernel(const float* __restrict__ dout,
                                                        float* __restrict__ dx, long long total,
                                                        int C, int M, long long P) {
-  const long long i = (long long)blockIdx.x * kHT + threadIdx.x;
-  if (i >= total) return;
-  const long long row = i / P;               // (n*M + m)*C + c
-  const int c = (int)(row % C);
-  const long long n = row / C / M;
-  // autograd's mean backward divides by a CPU scalar, which the device kernel turns into a
-  // multiply by the fp32 reciprocal: (dout * (1/M)) * (1/P)
-  dx[i] = (dout[n * C + c] * (1.f / (float)M)) * (1.f / (float)P);
+  const long long i0 = ((long long)blockIdx.x * kHT + threadIdx.x) * 4;
+  if (i0 >= total) return;
+  const float rm = 1.f / (float)M, rp = 1.f / (float)P;
+  float v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long long row = (i0 + u) / P;        // (n*M + m)*C + c
+    const int c = (int)(row % C);
+    const long long n = row / C / M;
+    // autograd's mean backward divides by a CPU scalar, which the device kernel turns into
+    // a multiply by the fp32 reciprocal: (dout * (1/M)) * (1/P)
+    v[u] = i0 + u < total ? (dout[n * C + c] * rm) * rp : 0.f;
+  }
+  if (i0 + 4 <= total) {
+    *reinterpret_cast<float4*>(dx + i0) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int u = 0; u < 4 && i0 + u < total; ++u) dx[i0 + u] = v[u];
+  }
 }
 
 unsigned grid1(long long total) { return (unsigned)((total + kHT - 1) / kHT); }
@@ -279,9 +291,10 @@ int sgcn_pool_bwd(const float* dout, float* dx, int N, int M, int C, long long P
   SGCN_REQUIRE(N >= 0 && M > 0 && C > 0 && P > 0);
   const long long total = (long long)N * M * C * P;
   if (total == 0) return 0;
-  SGCN_REQUIRE(dout && dx);
+  SGCN_REQUIRE(dout && dx && ((uintptr_t)dx & 15) == 0);   // 16-byte vector stores
   SGCN_REQUIRE(total < (1ll << 40));
-  pool_bwd_kernel<<<grid1(total), kHT, 0, (hipStream_t)stream>>>(dout, dx, total, C, M, P);
+  pool_bwd_kernel<<<grid1((total + 3) / 4), kHT, 0, (hipStream_t)stream>>>(dout, dx, total, C,
+                                                                           M, P);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

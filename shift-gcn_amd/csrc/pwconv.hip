@@ -822,35 +822,65 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
   }
 }
 
-// out[i] (+)= sum_s slab[s*n + i], i < n, in a FIXED order (deterministic): 64 outputs
-// per block, 4 split-groups of 64 threads each summing every 4th split with 8 loads in
-// flight, then the 4 group sums added in order. transpose: i = m*Nc + c -> out[c*M + m].
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab,
-                                                          int S, int n, int M, int Nc,
-                                                          float* __restrict__ out,
-                                                          int transpose, int accum) {
-  __shared__ float red[4][64];
+// Split-K reduction of the dW (and bias) slabs in ONE launch, FIXED order (deterministic):
+//   i <  n        : dw[i]     (+)= sum_s slab[s*n + i]        (transpose: i = m*Nc + c ->
+//                                                            stored at c*M + m)
+//   n <= i < n+nb : dbias[i-n] (+)= sum_s bslab[s*nb + i - n]
+// 64 outputs per block x 16 split-groups (1024 threads); a group sums every 16th split
+// with 16 loads in flight, then the 16 group sums are added in order. The slabs are a
+// few MB to 64 MB: few dependent load rounds per thread keep this launch short.
+constexpr int kRedGroups = 16, kRedU = 16;
+__global__ __launch_bounds__(64 * kRedGroups) void slab_reduce_kernel(
+    const float* __restrict__ slab, const float* __restrict__ bslab, int S, int n, int nb,
+    int M, int Nc, float* __restrict__ out, float* __restrict__ bout, int transpose,
+    int accum, int baccum) {
+  __shared__ float red[kRedGroups][64];
   const int il = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + il;
-  const int ic = min(i, n - 1);
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int s = q;
-  for (; s + 28 < S; s += 32) {
+  const bool isb = i >= n;
+  const float* __restrict__ src = isb ? bslab : slab;
+  const int stride = isb ? nb : n;
+  const int ic = isb ? min(i - n, nb - 1) : i;
+  float acc[kRedU];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] += slab[(size_t)(s + 4 * k) * n + ic];
-  }
-  for (; s < S; s += 4) acc[0] += slab[(size_t)s * n + ic];
-  red[q][il] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  __syncthreads();
-  if (q == 0 && i < n) {
-    const float tot = (red[0][il] + red[1][il]) + (red[2][il] + red[3][il]);
-    int dst = i;
-    if (transpose) {
-      const int m = i / Nc, c = i - m * Nc;
-      dst = c * M + m;
+  for (int k = 0; k < kRedU; ++k) acc[k] = 0.f;
+  if (i < n + nb) {
+    int s = q;
+    for (; s + kRedGroups * (kRedU - 1) < S; s += kRedGroups * kRedU) {
+#pragma unroll
+      for (int k = 0; k < kRedU; ++k) acc[k] += src[(size_t)(s + kRedGroups * k) * stride + ic];
     }
-    out[dst] = accum ? out[dst] + tot : tot;
+    for (; s < S; s += kRedGroups) acc[0] += src[(size_t)s * stride + ic];
   }
+#pragma unroll
+  for (int w = kRedU / 2; w >= 1; w >>= 1)
+#pragma unroll
+    for (int k = 0; k < w; ++k) acc[k] = acc[k] + acc[k + w];
+  red[q][il] = acc[0];
+  __syncthreads();
+  if (q == 0 && i < n + nb) {
+    float tot = 0.f;
+#pragma unroll
+    for (int g = 0; g < kRedGroups; ++g) tot += red[g][il];
+    if (isb) {
+      const int d = i - n;
+      bout[d] = baccum ? bout[d] + tot : tot;
+    } else {
+      int dst = i;
+      if (transpose) {
+        const int m = i / Nc, c = i - m * Nc;
+        dst = c * M + m;
+      }
+      out[dst] = accum ? out[dst] + tot : tot;
+    }
+  }
+}
+
+void launch_slab_reduce(const float* slab, const float* bslab, int S, int M, int Nc, float* dw,
+                        int transpose, int accum, float* dbias, int baccum, hipStream_t st) {
+  const int n = M * Nc, nb = dbias ? M : 0;
+  slab_reduce_kernel<<<(n + nb + 63) / 64, 64 * kRedGroups, 0, st>>>(
+      slab, bslab, S, n, nb, M, Nc, dw, dbias, transpose, accum, baccum);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1125,15 +1155,9 @@ int sgcn_pw_dw_tshift(const float* g, long long g_bstride, long long g_cstride, 
   a.mask_bytes = 0u;
   const int S = launch_dw3(a, st, slab, dbias != nullptr);
   SGCN_LAUNCH_CHECK();
-  const int MN = M * Nc;
-  slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(slab, S, MN, M, Nc, dw, dw_transpose,
-                                                    dw_accumulate);
+  launch_slab_reduce(slab, slab + (size_t)S * M * Nc, S, M, Nc, dw, dw_transpose, dw_accumulate,
+                     dbias, dbias_accumulate, st);
   SGCN_LAUNCH_CHECK();
-  if (dbias) {
-    slab_reduce_kernel<<<(M + 63) / 64, 256, 0, st>>>(slab + (size_t)S * M * Nc, S, M, M, 1,
-                                                     dbias, 0, dbias_accumulate);
-    SGCN_LAUNCH_CHECK();
-  }
   return 0;
 }
 
@@ -1188,15 +1212,9 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
 #undef SGCN_DW
   }
   SGCN_LAUNCH_CHECK();
-  const int MN = M * Nc;
-  slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(a.slab, S, MN, M, Nc, dw, dw_transpose,
-                                                    dw_accumulate);
+  launch_slab_reduce(a.slab, a.bslab, S, M, Nc, dw, dw_transpose, dw_accumulate, dbias,
+                     dbias_accumulate, st);
   SGCN_LAUNCH_CHECK();
-  if (dbias) {
-    slab_reduce_kernel<<<(M + 63) / 64, 256, 0, st>>>(a.bslab, S, M, M, 1, dbias, 0,
-                                                     dbias_accumulate);
-    SGCN_LAUNCH_CHECK();
-  }
   return 0;
 }
 

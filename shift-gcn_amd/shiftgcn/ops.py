@@ -25,8 +25,9 @@ class LaunchTimer:
     """Records (op, algorithmic flops, algorithmic bytes, start, end) for every C-ABI call
     made while active, with events on the stream the kernels are launched on."""
 
-    def __init__(self, ops_filter=None):
+    def __init__(self, ops_filter=None, detail=False):
         self.ops_filter = ops_filter
+        self.detail = detail      # key records by op + launch shape (tools/shape_breakdown.py)
         self.records = []
 
     def begin(self, op, flops, nbytes, device):
@@ -70,8 +71,13 @@ def set_launch_timer(timer):
 class _timed:
     __slots__ = ("rec",)
 
-    def __init__(self, op, flops, nbytes, t):
-        self.rec = _TIMER.begin(op, flops, nbytes, t.device) if _TIMER is not None else None
+    def __init__(self, op, flops, nbytes, t, detail=None):
+        if _TIMER is None:
+            self.rec = None
+            return
+        if _TIMER.detail and detail is not None:
+            op = f"{op} {detail}"
+        self.rec = _TIMER.begin(op, flops, nbytes, t.device)
 
     def __enter__(self):
         return self
@@ -80,6 +86,10 @@ class _timed:
         if self.rec is not None:
             _TIMER.end(self.rec)
         return False
+
+
+def _shp(t):
+    return "x".join(map(str, t.shape))
 
 
 def _stream(t: torch.Tensor):
@@ -125,7 +135,7 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
         out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
     lib = _lib.load()
     nb = 4 * (inp.numel() + out.numel())
-    with _timed("tshift_fwd", 0, nb, inp):
+    with _timed("tshift_fwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_fwd(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(scale),
                                  _ptr(shift), _ptr(stats), B, C, H, W, stride,
                                  int(ypos_is_raw), _stream(inp))
@@ -141,7 +151,7 @@ def _tshift_fwd_f64(inp, xpos, ypos, stride, ypos_is_raw, out=None):
     B, C, H, W = inp.shape
     if out is None:
         out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F64)
-    with _timed("tshift_fwd", 0, 8 * (inp.numel() + out.numel()), inp):
+    with _timed("tshift_fwd", 0, 8 * (inp.numel() + out.numel()), inp, _shp(inp)):
         rc = _lib.load().sgcn_tshift_fwd_f64(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), B,
                                              C, H, W, stride, int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_fwd_f64")
@@ -162,7 +172,7 @@ def _tshift_bwd_f64(gout, inp, xpos, ypos, stride, ypos_is_raw):
     gy = torch.empty((C,), device=dev, dtype=_F64)
     nbytes = lib.sgcn_tshift_bwd_f64_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 8) + 7) // 8, device=dev, dtype=_F64)
-    with _timed("tshift_bwd", 0, 8 * (gout.numel() + 2 * inp.numel()), inp):
+    with _timed("tshift_bwd", 0, 8 * (gout.numel() + 2 * inp.numel()), inp, _shp(inp)):
         rc = lib.sgcn_tshift_bwd_f64(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos), _ptr(gin),
                                      _ptr(gx), _ptr(gy), _ptr(ws), nbytes, B, C, H, W, stride,
                                      int(ypos_is_raw), _stream(inp))
@@ -181,7 +191,7 @@ def tshift_fwd_pre(z, xpos, ypos, stride, zst, r, rst, ast):
     B, C, H, W = z.shape
     out = torch.empty((B, C, H // stride, W), device=z.device, dtype=_F32)
     nb = 4 * (2 * z.numel() + out.numel())
-    with _timed("tshift_fwd", 0, nb, z):
+    with _timed("tshift_fwd", 0, nb, z, _shp(z)):
         rc = _lib.load().sgcn_tshift_fwd_pre(
             _ptr(z), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(zst.scale), _ptr(zst.shift),
             _ptr(r), _ptr(rst.scale) if rst else None, _ptr(rst.shift) if rst else None,
@@ -200,7 +210,7 @@ def tshift_fwd_tail(inp, xpos, ypos, stride, st, r=None, rst=None, gather_m=None
     out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
     og = torch.empty_like(out) if gather_m is not None else None
     nb = 4 * (inp.numel() + out.numel() * (1 + (r is not None) + (og is not None)))
-    with _timed("tshift_fwd", 0, nb, inp):
+    with _timed("tshift_fwd", 0, nb, inp, _shp(inp)):
         rc = _lib.load().sgcn_tshift_fwd_tail(
             _ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(st.scale), _ptr(st.shift),
             _ptr(r), _ptr(rst.scale) if rst else None, _ptr(rst.shift) if rst else None,
@@ -233,7 +243,7 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
     bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if bn_stats is not None else None
     nb = 4 * (gout.numel() + 2 * inp.numel())
-    with _timed("tshift_bwd", 0, nb, inp):
+    with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_bwd(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos), _ptr(scale),
                                  _ptr(shift), int(bool(relu_mask)),
                                  _ptr(bn_stats.mean) if bn_stats is not None else None,
@@ -261,7 +271,7 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos):
     gy = torch.empty((C,), device=dev, dtype=_F32)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
-    with _timed("tshift_bwd", 0, 4 * (3 * dy.numel() + 2 * inp.numel()), inp):
+    with _timed("tshift_bwd", 0, 4 * (3 * dy.numel() + 2 * inp.numel()), inp, _shp(inp)):
         rc = lib.sgcn_tshift_bwd_bnin(_ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp),
                                       _ptr(xpos), _ptr(ypos), _ptr(gin), _ptr(gx), _ptr(gy),
                                       _ptr(ws), nbytes, B, C, H, W, 1, _stream(inp))
@@ -321,7 +331,10 @@ def pw_fwd(w, w_mcontig, bias, x: PlaneView, out: PlaneView, M, K, T, V, mask=No
     lib = _lib.load()
     P = B * T * V
     bc = _batch_chunk([(x, K), (out, M)], B, T, V)
-    with _timed("pw_fwd", 2.0 * P * M * K, 4.0 * P * (M * (2 if accumulate else 1) + K), x.t):
+    det = (f"M{M} K{K} T{T} V{V} xrot{x.rsign} yrot{out.rsign} mask{int(mask is not None)} "
+           f"ts{x.tstride}{out.tstride} acc{int(accumulate)} mc{int(w_mcontig)}")
+    with _timed("pw_fwd", 2.0 * P * M * K, 4.0 * P * (M * (2 if accumulate else 1) + K), x.t,
+                det):
         for b0 in range(0, B, bc):
             nb = min(bc, B - b0)
             rc = lib.sgcn_pw_fwd(_ptr(w), int(w_mcontig), _ptr(bias),
@@ -344,7 +357,9 @@ def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=Fals
     nbytes = lib.sgcn_pw_dw_ws_bytes(bc, M, Nc, T, V)
     ws = torch.empty((nbytes + 3) // 4, device=g.t.device, dtype=_F32)
     P = B * T * V
-    with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t):
+    det = (f"M{M} N{Nc} T{T} V{V} grot{g.rsign} xrot{x.rsign} mask{int(mask is not None)} "
+           f"ts{g.tstride}{x.tstride}")
+    with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t, det):
         for b0 in range(0, B, bc):
             nb = min(bc, B - b0)
             first = b0 == 0
@@ -382,7 +397,8 @@ def pw_fwd_tshift(w, bias, x: PlaneView, xpos, ypos, st, out: PlaneView, M, K, T
         if x_shifted.shape != x.t.shape or x_shifted.stride() != x.t.stride():
             raise ValueError("x_shifted must have the layout of x")
     nbx = 4.0 * P * (M + K * (2 if x_shifted is not None else 1))
-    with _timed("pw_fwd", 2.0 * P * M * K, nbx, x.t):
+    with _timed("pw_fwd", 2.0 * P * M * K, nbx, x.t,
+                f"TSH M{M} K{K} T{T} V{V} side{int(x_shifted is not None)}"):
         for b0 in range(0, B, bc):
             nb = min(bc, B - b0)
             xs = None if x_shifted is None else x_shifted.data_ptr() + 4 * b0 * x.bstride
@@ -410,7 +426,7 @@ def pw_dw_tshift(g: PlaneView, x: PlaneView, xpos, ypos, st, dw, M, Nc, T, V, db
     P = B * T * V
     sc = st.scale if st is not None else None
     sh = st.shift if st is not None else None
-    with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t):
+    with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t, f"TSH M{M} N{Nc} T{T} V{V}"):
         for b0 in range(0, B, bc):
             nb = min(bc, B - b0)
             first = b0 == 0
@@ -430,7 +446,7 @@ def moments(x, per_joint):
     check_input(x, "input")
     B, C, T, V = x.shape
     part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=x.device, dtype=_F32)
-    with _timed("bn_stats", 0, 4 * x.numel(), x):
+    with _timed("bn_stats", 0, 4 * x.numel(), x, _shp(x)):
         rc = _lib.load().sgcn_moments(_ptr(x), _ptr(part), B, C, T, V, int(per_joint),
                                       _stream(x))
     _lib.check(rc, "sgcn_moments")
@@ -494,7 +510,7 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
     ys = torch.empty((B * C * 2,), device=x.device, dtype=_F32) if out_stats else None
     yg = torch.empty_like(y) if gather_m is not None else None
     nb = 4 * x.numel() * (2 + (r is not None) + (yg is not None))
-    with _timed("bn_apply", 0, nb, x):
+    with _timed("bn_apply", 0, nb, x, _shp(x)):
         rc = _lib.load().sgcn_bn_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift),
                                        int(per_joint), _ptr(r),
                                        _ptr(rst.scale) if rst else None,
@@ -515,7 +531,7 @@ def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats =
     part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=dev, dtype=_F32)
     rpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if r is not None else None
     nb = 4 * x.numel() * (2 + (y is not None) + (r is not None))
-    with _timed("bn_bwd_reduce", 0, nb, x):
+    with _timed("bn_bwd_reduce", 0, nb, x, _shp(x)):
         rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x),
                                             _ptr(st.mean), _ptr(st.invstd), int(per_joint),
                                             _ptr(r), _ptr(rst.mean) if rst else None,
@@ -545,7 +561,7 @@ def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, d
     B, C, T, V = x.shape
     dx = torch.empty_like(x) if dx is None else dx
     nb = 4 * x.numel() * (3 + (y is not None) + (r is not None) + (dr is not None))
-    with _timed("bn_bwd_apply", 0, nb, x):
+    with _timed("bn_bwd_apply", 0, nb, x, _shp(x)):
         rc = _lib.load().sgcn_bn_bwd_apply(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(coef),
                                            int(per_joint), _ptr(r), _ptr(rcoef),
                                            _ptr(dy_coef), _ptr(dx), _ptr(dr), B, C, T, V,
@@ -566,7 +582,7 @@ def mask_prep(mask):
 def gcn_gather(x0, m):
     B, C, T, V = x0.shape
     xg = torch.empty_like(x0)
-    with _timed("gcn_gather", 0, 8 * x0.numel(), x0):
+    with _timed("gcn_gather", 0, 8 * x0.numel(), x0, _shp(x0)):
         rc = _lib.load().sgcn_gcn_gather(_ptr(x0), _ptr(m), _ptr(xg), B, C, T, V,
                                          _stream(x0))
     _lib.check(rc, "sgcn_gcn_gather")
@@ -582,7 +598,7 @@ def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
     pp = torch.empty((B * C * 2,), device=dxt.device, dtype=_F32) if prev is not None else None
     ps, pst = prev if prev is not None else (None, None)
     nb = 4 * dxt.numel() * (3 + sum(t is not None for t in (add1, add2, add2_mask, ps)))
-    with _timed("gcn_dx_finish", 0, nb, dxt):
+    with _timed("gcn_dx_finish", 0, nb, dxt, _shp(dxt)):
         rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1),
                                             _ptr(add2), _ptr(add2_mask), _ptr(dx), _ptr(part),
                                             _ptr(ps), _ptr(pst.mean) if pst else None,

@@ -10,8 +10,9 @@ model/shift_gcn.py:66-69, shift_cuda_kernel.cu:11-76).
 * the side output (mode 1, default) is the shifted operand, element for element;
 * every fusion mode (0: two launches, 1: fused + side output, 2: the weight gradient re-forms
   the operand) gives the same unit parity vs the oracle;
-* in a training step there is no separate shift_in launch: the only temporal-shift forward
-  launches left are the 10 shift_outs (whose output feeds bn2's statistics).
+* in a training step there is no separate shift_in launch for the units at or above the
+  channel threshold: the other temporal-shift forward launches are the 10 shift_outs
+  (whose output feeds bn2's statistics).
 """
 import numpy as np
 import pytest
@@ -121,11 +122,16 @@ def test_unit_matches_oracle_in_every_fusion_mode(monkeypatch, mode):
     _compare(ref, ours, xr, yr, xo, yo, f"mode{mode}")
 
 
-def test_training_step_has_no_shift_in_launch(monkeypatch):
+@pytest.mark.parametrize("min_c", [0, None])
+def test_training_step_has_no_shift_in_launch(monkeypatch, min_c):
+    """Every unit at or above the channel threshold (SGCN_TSHIFT_FUSION_MIN_C; 0 = all)
+    runs shift_in inside its contraction; units below it keep the two-launch form."""
     import formula
     import shiftgcn
     from shiftgcn import fused, ops
     assert fused.TSHIFT_FUSION
+    if min_c is not None:
+        monkeypatch.setattr(fused, "TSHIFT_FUSION_MIN_C", min_c)
     calls = {"affine": 0, "plain": 0}
     real = ops.tshift_fwd
 
@@ -139,4 +145,6 @@ def test_training_step_has_no_shift_in_launch(monkeypatch):
     x = formula.tensor((2, 3, 16, 25, 2), 5, 1.0).to(DEV)
     m(x).sum().backward()
     torch.cuda.synchronize()
-    assert calls == {"affine": 0, "plain": 10}, calls
+    unfused = sum(getattr(m, f"l{k}").tcn1.in_channels < fused.TSHIFT_FUSION_MIN_C
+                  for k in range(1, 11))
+    assert calls == {"affine": unfused, "plain": 10}, calls

@@ -54,7 +54,7 @@ void dw_variant(const char* name, const Shape& s, DwArgs a, int S, hipStream_t s
   auto L = [&]() {
     if (s.mask) pw_dw_kernel<BM, BN, WM, WN, true><<<grid, 64 * WM * WN, dyn, st>>>(a);
     else pw_dw_kernel<BM, BN, WM, WN, false><<<grid, 64 * WM * WN, 0, st>>>(a);
-    slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(a.slab, S, MN, a.M, a.Nc, dwout, 0, 0);
+    launch_slab_reduce(a.slab, nullptr, S, a.M, a.Nc, dwout, 0, 0, nullptr, 0, st);
   };
   float us = timeit(L, st, 10);
   printf("%-20s %-26s S=%5d %8.1f us  %6.1f TF/s  %6.2f TB/s  %s\n", s.name, name, S, us,
@@ -164,7 +164,7 @@ int main(int argc, char** argv) {
       const int MN = s.M * s.K;
       auto L3 = [&]() {
         S3 = launch_dw3(d3, st, ws, false);
-        slab_reduce_kernel<<<(MN + 63) / 64, 256, 0, st>>>(ws, S3, MN, s.M, s.K, dw2, 0, 0);
+        launch_slab_reduce(ws, nullptr, S3, s.M, s.K, dw2, 0, 0, nullptr, 0, st);
       };
       float us = timeit(L3, st, 10);
       std::vector<float> h1(MN), h2(MN);
