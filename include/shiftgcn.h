@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 14
+#define SGCN_ABI_VERSION 15
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -121,6 +121,24 @@ int sgcn_tshift_bwd_f64(const double* gout, const double* in, const double* xpos
                         const double* ypos, double* gin, double* gx, double* gy, void* ws,
                         size_t ws_bytes, int B, int C, int H, int W, int stride,
                         int ypos_is_raw, void* stream);
+
+/* Shift_tcn.shift_in backward inside a TCN_GCN_unit whose Shift_gcn has no down conv
+ * (shift_gcn.py:137-141 then :66-68): exactly sgcn_tshift_bwd(stride 1, in_scale/in_shift,
+ * bn_mean/bn_invstd/bn_part) — same gin, gx, gy, bn_part — and in the same launch the
+ * k-free backward sums of Shift_gcn.bn (the per-joint BatchNorm1d whose ReLU output is
+ * `in`): z_part[j][b*C*W + c*W + w], j = {sum gin, sum (in - mu), sum 1, sum gin*zh,
+ * sum (in - mu)*zh, sum zh} over t where in > 0, zh = (z - z_mean[c*W+w]) *
+ * z_invstd[c*W+w], mu = bn_mean[c]; z = that BatchNorm's input (the gcn contraction
+ * output), statistics in the per-joint local order. Feed z_part to
+ * sgcn_bn_bwd_finalize_gbn; no separate sgcn_bn_bwd_reduce pass over (gin, in, z).
+ * H*W <= 16384 and W <= 256 only (else SGCN_EINVAL: use sgcn_tshift_bwd +
+ * sgcn_bn_bwd_reduce). */
+int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
+                        const float* ypos, const float* in_scale, const float* in_shift,
+                        const float* bn_mean, const float* bn_invstd, float* bn_part,
+                        const float* z, const float* z_mean, const float* z_invstd,
+                        float* z_part, float* gin, float* gx, float* gy, void* ws,
+                        size_t ws_bytes, int B, int C, int H, int W, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Pointwise (1x1) channel contraction with the joint-shift gathers fused (fp32 MFMA)
@@ -245,6 +263,17 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
                          const float* mean, const float* invstd, const float* gamma,
                          float* dgamma, float* dbeta, int accumulate, int batch_stats,
                          float* coef, void* stream);
+
+/* sgcn_bn_bwd_finalize for the per-joint BatchNorm1d (F = C*V features, perm_V = V) from
+ * the six k-free sums of sgcn_tshift_bwd_gbn: g = k1*gin + k2*(in - mu) + (k3 + k2*mu)
+ * with dy_coef = [3][C] {k1,k2,k3} (the following BatchNorm's sgcn_bn_bwd_finalize
+ * coefficients) and dy_mean = [C] its mean mu (any centring value is exact; the batch
+ * mean avoids cancellation); then dgamma/dbeta/coef exactly as sgcn_bn_bwd_finalize. */
+int sgcn_bn_bwd_finalize_gbn(const float* part6, int B, int C, int V, long long n_total,
+                             const float* dy_coef, const float* dy_mean, const float* mean,
+                             const float* invstd, const float* gamma, float* dgamma,
+                             float* dbeta, int accumulate, int batch_stats, float* coef,
+                             void* stream);
 
 /* dx = k1*g + k2*x + k3; dr = g (rcoef NULL, dr given) or rk1*g + rk2*r + rk3;
  * dy_coef as in sgcn_bn_bwd_reduce. per_joint = 2: per-joint coefficients AND dx written

@@ -390,6 +390,65 @@ __global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
   coef[2 * F + f] = k3;
 }
 
+// The same from the k-free per-(plane, joint) sums of sgcn_tshift_bwd_gbn:
+//   part6[j][b][f], j = {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh}
+// over the active (H > 0) positions, g = k1*dA + k2*(H - mu) + (k3 + k2*mu) with
+// k = dyc[3][C] (Shift_tcn.bn's backward coefficients) and mu = dym[C] (its batch mean),
+// channel c = f / V. The six sums are merged over b in double (32 features x 16 slices,
+// fixed order), then combined once per feature.
+constexpr int kSl6 = 16;
+__global__ __launch_bounds__(kFeat * kSl6) void bn_bwd_finalize_gbn_kernel(
+    const float* __restrict__ part6, int B, int F, int V, double n_total,
+    const float* __restrict__ dyc, const float* __restrict__ dym, int C,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    int accumulate, int batch_stats, float* __restrict__ coef) {
+  __shared__ double l6[6][kSl6][kFeat];
+  const int fl = threadIdx.x % kFeat, q = threadIdx.x / kFeat;
+  const int f = blockIdx.x * kFeat + fl;
+  const int fc = min(f, F - 1);
+  const size_t np = (size_t)B * F;
+  double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int b0 = q; b0 < B; b0 += kSl6 * 8) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u * kSl6;
+        pv[u] = b < B ? part6[j * np + (size_t)b * F + fc] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[j] += pv[u];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) l6[j][q][fl] = a[j];
+  __syncthreads();
+  if (q != 0 || f >= F) return;
+  double s6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < kSl6; ++k)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s6[j] += l6[j][k][fl];
+  const int c = f / V;
+  const double k1 = dyc[c], k2 = dyc[C + c], c3 = (double)dyc[2 * C + c] + k2 * (double)dym[c];
+  const double sg = k1 * s6[0] + k2 * s6[1] + c3 * s6[2];
+  const double sgx = k1 * s6[3] + k2 * s6[4] + c3 * s6[5];
+  const int rf = ref_feature(f, V, F);
+  if (dgamma) dgamma[rf] = accumulate ? dgamma[rf] + (float)sgx : (float)sgx;
+  if (dbeta) dbeta[rf] = accumulate ? dbeta[rf] + (float)sg : (float)sg;
+  const float g = gamma ? gamma[rf] : 1.f;
+  const float is = invstd[f];
+  const float q1 = g * is;
+  // running-statistics (eval) BatchNorm: dx = q1 * g, as bn_bwd_finalize_kernel
+  const float q2 = batch_stats ? (float)(-(double)q1 * (double)is * (sgx / n_total)) : 0.f;
+  const float q3 = batch_stats ? (float)(-(double)q1 * (sg / n_total) - (double)q2 * (double)mean[f])
+                               : 0.f;
+  coef[f] = q1;
+  coef[F + f] = q2;
+  coef[2 * F + f] = q3;
+}
+
 // dx = k1[f]*g + k2[f]*x + k3[f]; RES: 1 -> dr = g, 2 -> dr = rk1*g + rk2*r + rk3
 // PJM: 0 per-channel, 1 per-joint, 2 per-joint with dx stored GATHERED: element (c, t, v)
 // goes to (c, t, (v - c) mod V), i.e. the shift_out gather of the next contraction
@@ -737,6 +796,21 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
   bn_bwd_finalize_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSlices, 0, (hipStream_t)stream>>>(
       (const float2*)part, B, F, (double)n_total, perm_V, mean, invstd, gamma, dgamma, dbeta,
+      accumulate, batch_stats, coef);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_bn_bwd_finalize_gbn(const float* part6, int B, int C, int V, long long n_total,
+                             const float* dy_coef, const float* dy_mean, const float* mean,
+                             const float* invstd, const float* gamma, float* dgamma,
+                             float* dbeta, int accumulate, int batch_stats, float* coef,
+                             void* stream) {
+  SGCN_REQUIRE(part6 && B > 0 && C > 0 && V > 0 && n_total > 0 && dy_coef && dy_mean && mean &&
+               invstd && coef);
+  const int F = C * V;
+  bn_bwd_finalize_gbn_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSl6, 0, (hipStream_t)stream>>>(
+      part6, B, F, V, (double)n_total, dy_coef, dy_mean, C, mean, invstd, gamma, dgamma, dbeta,
       accumulate, batch_stats, coef);
   SGCN_LAUNCH_CHECK();
   return 0;

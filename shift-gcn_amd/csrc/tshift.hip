@@ -522,7 +522,18 @@ __global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
 // formed while staging: gout = k1*(gy > 0 ? gdy : 0) + k2*gx + k3 (gdy = the unit's output
 // gradient, gy = its output, gx = bn2's input S, k = sgcn_bn_bwd_finalize coefficients),
 // so that gradient tensor is never written.
-template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP, bool GP = false>
+//
+// GBN (stride 1, with AFFINE + BNP: Shift_tcn's shift_in inside a TCN_GCN_unit whose
+// Shift_gcn has no down conv): also the backward partials of Shift_gcn.bn, the per-joint
+// BatchNorm1d whose ReLU output H is this shift's input (shift_gcn.py:137-141), without a
+// separate pass over (dA, H, Z). Its input gradient is g = [H > 0] * (k1*dA + k2*H + k3)
+// with k = Shift_tcn.bn's backward coefficients, which need this launch's own batch-wide
+// partials first; so the k-free sums are emitted per (plane, joint) instead, centred on
+// Shift_tcn.bn's mean mu (k2*H + k3 = k2*(H - mu) + (k3 + k2*mu), no cancellation):
+//   {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh} over t where H > 0,
+//   zh = (Z - zmean[c,v]) * zinvstd[c,v]; sgcn_bn_bwd_finalize_gbn combines them.
+template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP, bool GP = false,
+          bool GBN = false>
 __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
@@ -531,8 +542,11 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
     int Hb, int W, int Ho, int add_half, const float* __restrict__ gdy = nullptr,
     const float* __restrict__ gy = nullptr, const float* __restrict__ gx = nullptr,
-    const float* __restrict__ gcoef = nullptr) {
+    const float* __restrict__ gcoef = nullptr, const float* __restrict__ gz = nullptr,
+    const float* __restrict__ gzm = nullptr, const float* __restrict__ gzi = nullptr,
+    float* __restrict__ gzpart = nullptr) {
   static_assert(!GP || STRIDE == 1, "GP is a stride-1 (re-associated) variant");
+  static_assert(!GBN || (STRIDE == 1 && BNP && !GP), "GBN: stride-1 shift_in with BNP");
   // STRIDE == 1 ("re-associated"): only gout is staged (half the LDS -> twice the
   // workgroups per CU); each thread's own input elements are loaded into registers with
   // the staging loads, and the position-gradient sums are accumulated over INPUT positions
@@ -607,6 +621,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   // (1) grad_input over the bottom grid (.cu:108-150 stride 1; .cu:191-254 stride 2)
   float bs0 = 0.f, bs1 = 0.f;
   float ax = 0.f, ay = 0.f;
+  float dav[GBN ? LPT : 1];   // GBN: this thread's input gradients, for the joint partials
   if (RA) {
     const Geom r = make_geom(-x, -y);
     const Geom g = make_geom(x, y);
@@ -623,6 +638,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
         const float rin = rin_r[e];
         if (RELU_MASK) val = rin > 0.f ? val : 0.f;
         gi[o] = val;
+        if (GBN) dav[e] = val;
         if (BNP) {
           bs0 += val;
           bs1 += val * ((rin - bmu) * bis);
@@ -702,6 +718,112 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   if (BNP) {
     block_sum2(bs0, bs1, red);
     if (threadIdx.x == 0) bn_part[plane] = make_float2(bs0, bs1);
+  }
+  if (GBN) {
+    __syncthreads();   // every LDS read of gout is done: the plane's dA goes there instead
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int o = e * NT + threadIdx.x;
+      if (o < nb) lds[o] = dav[e];
+    }
+    __syncthreads();
+    // per joint: thread (v, row group r) walks rows r, r + G, ... (coalesced H/Z rows)
+    const int G = NT / W;
+    float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if ((int)threadIdx.x < G * W) {
+      const int v = threadIdx.x % W, r = threadIdx.x / W;
+      const float zm = gzm[c * W + v], zi = gzi[c * W + v];
+      const float* __restrict__ hp = in + (size_t)plane * nb;
+      const float* __restrict__ zp = gz + (size_t)plane * nb;
+      for (int t0 = r; t0 < Hb; t0 += 4 * G) {
+        float hv[4], zv[4], dv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int o = min(t0 + u * G, Hb - 1) * W + v;
+          hv[u] = hp[o];
+          zv[u] = zp[o];
+          dv[u] = lds[o];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (t0 + u * G < Hb && hv[u] > 0.f) {
+            const float hc = hv[u] - bmu, zh = (zv[u] - zm) * zi;
+            a6[0] += dv[u];
+            a6[1] += hc;
+            a6[2] += 1.f;
+            a6[3] += dv[u] * zh;
+            a6[4] += hc * zh;
+            a6[5] += zh;
+          }
+        }
+      }
+    }
+    __syncthreads();   // dA reads done: the LDS now holds the 6 x NT per-thread sums
+#pragma unroll
+    for (int k = 0; k < 6; ++k) lds[k * NT + threadIdx.x] = a6[k];
+    __syncthreads();
+    if ((int)threadIdx.x < W) {
+      const size_t np = (size_t)gridDim.x * W;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        float sum = 0.f;
+        for (int g = 0; g < G; ++g) sum += lds[k * NT + g * W + threadIdx.x];
+        gzpart[k * np + (size_t)plane * W + threadIdx.x] = sum;
+      }
+    }
+  }
+  if (GBN) {
+    __syncthreads();   // every LDS read of gout is done: the plane's dA goes there instead
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int o = e * NT + threadIdx.x;
+      if (o < nb) lds[o] = dav[e];
+    }
+    __syncthreads();
+    // per joint: thread (v, row group r) walks rows r, r + G, ... (coalesced H/Z rows)
+    const int G = NT / W;
+    float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if ((int)threadIdx.x < G * W) {
+      const int v = threadIdx.x % W, r = threadIdx.x / W;
+      const float zm = gzm[c * W + v], zi = gzi[c * W + v];
+      const float* __restrict__ hp = in + (size_t)plane * nb;
+      const float* __restrict__ zp = gz + (size_t)plane * nb;
+      for (int t0 = r; t0 < Hb; t0 += 4 * G) {
+        float hv[4], zv[4], dv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int o = min(t0 + u * G, Hb - 1) * W + v;
+          hv[u] = hp[o];
+          zv[u] = zp[o];
+          dv[u] = lds[o];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (t0 + u * G < Hb && hv[u] > 0.f) {
+            const float hc = hv[u] - bmu, zh = (zv[u] - zm) * zi;
+            a6[0] += dv[u];
+            a6[1] += hc;
+            a6[2] += 1.f;
+            a6[3] += dv[u] * zh;
+            a6[4] += hc * zh;
+            a6[5] += zh;
+          }
+        }
+      }
+    }
+    __syncthreads();   // dA reads done: the LDS now holds the 6 x NT per-thread sums
+#pragma unroll
+    for (int k = 0; k < 6; ++k) lds[k * NT + threadIdx.x] = a6[k];
+    __syncthreads();
+    if ((int)threadIdx.x < W) {
+      const size_t np = (size_t)gridDim.x * W;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        float sum = 0.f;
+        for (int g = 0; g < G; ++g) sum += lds[k * NT + g * W + threadIdx.x];
+        gzpart[k * np + (size_t)plane * W + threadIdx.x] = sum;
+      }
+    }
   }
 }
 
@@ -1005,6 +1127,42 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
 }
 
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C) { return (size_t)B * C * sizeof(float2); }
+
+int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
+                        const float* ypos, const float* in_scale, const float* in_shift,
+                        const float* bn_mean, const float* bn_invstd, float* bn_part,
+                        const float* z, const float* z_mean, const float* z_invstd,
+                        float* z_part, float* gin, float* gx, float* gy, void* ws,
+                        size_t ws_bytes, int B, int C, int H, int W, void* stream) {
+  SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && W <= 256);
+  SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
+  SGCN_REQUIRE(gout && in && xpos && ypos && in_scale && in_shift && bn_mean && bn_invstd &&
+               bn_part && z && z_mean && z_invstd && z_part && gin && gx && gy && ws);
+  SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
+  SGCN_REQUIRE((long long)B * C < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  float2* pg = (float2*)ws;
+  float2* bp = (float2*)bn_part;
+#define SGCN_GBN(NT, L)                                                                        \
+  tshift_bwd_lds_kernel<NT, L, true, false, 1, true, false, true>                               \
+      <<<B * C, NT, (size_t)max(H * W, 6 * NT) * sizeof(float), st>>>(                          \
+          gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, C, H, W,   \
+          H, 0, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part)
+  // same thread/LPT choice as sgcn_tshift_bwd's stride-1 LDS path
+  if (H * W <= 2048) SGCN_GBN(256, 8);
+  else if (H * W <= 4096) SGCN_GBN(256, 16);
+  else {
+    const int lpt = pick_lpt(H * W, kBwdThreads);
+    if (lpt == 8) SGCN_GBN(kBwdThreads, 8);
+    else if (lpt == 16) SGCN_GBN(kBwdThreads, 16);
+    else SGCN_GBN(kBwdThreads, 32);
+  }
+#undef SGCN_GBN
+  SGCN_LAUNCH_CHECK();
+  tshift_pos_finalize_kernel<<<(C + 31) / 32, 1024, 0, st>>>(pg, B, C, gx, gy);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
 
 int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const float* ypos,
                     const float* in_scale, const float* in_shift, int relu_mask,

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen: one HIP runtime per proces
 
 LIB_NAME = "libshiftgcn_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-ABI_VERSION = 14
+ABI_VERSION = 15
 EINVAL = -22
 
 _lib = None
@@ -71,6 +71,10 @@ SIGNATURES = {
                                   _I, _I, _P]),
     "sgcn_mask_grad_finalize": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "sgcn_modalities": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "sgcn_tshift_bwd_gbn": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                 _P, _Z, _I, _I, _I, _I, _P]),
+    "sgcn_bn_bwd_finalize_gbn": (_I, [_P, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _I,
+                                      _P, _P]),
     "sgcn_head_ws_bytes": (_Z, [_I, _I, _I, _I]),
     "sgcn_head_moments": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "sgcn_head_apply": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),

@@ -83,25 +83,34 @@ def gcn_forward(mod, x0, training):
     return H, s
 
 
-def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, extra_out=None):
+def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, extra_out=None,
+                 pre6=None):
     """Returns (dx0, {param_name: grad}). With ``dy_coef`` ([3, Cout]) the incoming
     gradient is dH = k1*dH_arg + k2*H + k3 (Shift_tcn.bn's input gradient), evaluated
-    on the fly by the BN-backward kernels instead of being materialised."""
+    on the fly by the BN-backward kernels instead of being materialised. ``pre6`` =
+    (six-sum partials, Shift_tcn.bn stats) from sgcn_tshift_bwd_gbn: bn's backward
+    partials were made by the shift_in backward launch (no reduce pass here)."""
     x0 = s.x0
     B, Cin, T, V = x0.shape
     Cout = mod.out_channels
     g = {}
-    if mod.has_down:
-        conv, bnd = mod.down[0], mod.down[1]
-        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, r=s.D0, rst=s.dst,
-                                        dy_coef=dy_coef)
+    if pre6 is not None:
+        assert dy_coef is not None and not mod.has_down
+        coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize_gbn(
+            pre6[0], B, Cout, V, B * T, dy_coef, pre6[1], s.zst, mod.bn)
     else:
-        part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, dy_coef=dy_coef)
-    coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, Cout * V, B * T, s.zst,
-                                                               mod.bn, perm_V=V)
+        if mod.has_down:
+            conv, bnd = mod.down[0], mod.down[1]
+            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, r=s.D0,
+                                            rst=s.dst, dy_coef=dy_coef)
+        else:
+            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, dy_coef=dy_coef)
+        coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, Cout * V, B * T,
+                                                                   s.zst, mod.bn, perm_V=V)
     dZ = _empty(B, Cout, T, V, like=x0)
     g_id = dD0 = None
     if mod.has_down:
+        conv, bnd = mod.down[0], mod.down[1]
         coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
             rpart, B, Cout, B * T * V, s.dst, bnd)
         dD0 = _empty(B, Cout, T, V, like=x0)
@@ -215,9 +224,12 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
     return S, sst, s
 
 
-def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None):
+def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_z=None,
+                      out=None):
     """dS: gradient w.r.t. S (pre-bn2). Returns (dH, grads), or ((dA, coef), grads) with
-    ``materialize_dx=False`` (dH = coef[0]*dA + coef[1]*H + coef[2], fused downstream)."""
+    ``materialize_dx=False`` (dH = coef[0]*dA + coef[1]*H + coef[2], fused downstream).
+    ``gcn_z`` = (Z, zst) of the producing Shift_gcn (no down conv): its BatchNorm's
+    backward sums come out of the shift_in backward launch, returned as out["pre6"]."""
     H = s.H
     B, C, T, V = H.shape
     Cout = mod.out_channels
@@ -240,10 +252,17 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None):
     g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
     dAs = _empty(B, C, T, V, like=H)
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
-    # shift_in backward with Shift_tcn.bn's backward partials fused in
-    dA, g["shift_in.xpos"], g["shift_in.ypos"], part = ops.tshift_bwd(
-        dAs, H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=s.ast.scale,
-        shift=s.ast.shift, bn_stats=s.ast)
+    # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
+    # the Shift_gcn BatchNorm that produced H)
+    if (gcn_z is not None and GBN_FUSION and si.stride == 1 and V <= 256 and
+            T * V <= ops.GBN_MAX_PLANE):
+        dA, g["shift_in.xpos"], g["shift_in.ypos"], part, zpart = ops.tshift_bwd_gbn(
+            dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0], gcn_z[1])
+        out["pre6"] = (zpart, s.ast)
+    else:
+        dA, g["shift_in.xpos"], g["shift_in.ypos"], part = ops.tshift_bwd(
+            dAs, H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=s.ast.scale,
+            shift=s.ast.shift, bn_stats=s.ast)
     coef, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, C, B * T * V, s.ast,
                                                              mod.bn)
     if not materialize_dx:
@@ -346,6 +365,12 @@ def unit_forward(unit, x, training):
     return out, s
 
 
+def _gcn_z(unit, s: UnitSaved):
+    """(Z, zst) of the unit's Shift_gcn when its BatchNorm's backward sums can come out of
+    the shift_in backward launch (no down conv: its BN would need another input)."""
+    return None if unit.gcn1.has_down else (s.gs.Z, s.gs.zst)
+
+
 def unit_backward(unit, s: UnitSaved, dout):
     ts = s.ts
     S = ts.S
@@ -366,14 +391,16 @@ def unit_backward(unit, s: UnitSaved, dout):
             S.shape[2] * S.shape[3] <= ops.BNIN_MAX_PLANE):
         # neither dS nor the identity-residual gradient is written: the shift_out backward
         # forms dS while staging, gcn_dx_finish forms dout*(out > 0)
+        fo = {}
         (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, None, materialize_dx=False,
-                                            gpre=(dout, s.out, coef2))
+                                            gpre=(dout, s.out, coef2), gcn_z=_gcn_z(unit, s),
+                                            out=fo)
         g.update({"tcn1." + k: v for k, v in gt.items()})
         extra = {}
         dx, gg = gcn_backward(unit.gcn1, s.gs, dA,
                               extra_dx=(dout, s.out) if kind == "identity" else None,
                               dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
-                              extra_out=extra)
+                              extra_out=extra, pre6=fo.get("pre6"))
         if s.prev is not None:
             s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
         g.update({"gcn1." + k: v for k, v in gg.items()})
@@ -391,12 +418,14 @@ def unit_backward(unit, s: UnitSaved, dout):
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dr=dres, dx=dS)
     else:
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dx=dS)
-    (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, dS, materialize_dx=False)
+    fo = {}
+    (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, dS, materialize_dx=False,
+                                        gcn_z=_gcn_z(unit, s), out=fo)
     g.update({"tcn1." + k: v for k, v in gt.items()})
     extra = {}
     dx, gg = gcn_backward(unit.gcn1, s.gs, dA, extra_dx=dres if kind == "identity" else None,
                           dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
-                          extra_out=extra)
+                          extra_out=extra, pre6=fo.get("pre6"))
     if s.prev is not None:   # kind != "conv" and no gcn down conv: dx is final here
         s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
     g.update({"gcn1." + k: v for k, v in gg.items()})
@@ -416,6 +445,9 @@ def unit_backward(unit, s: UnitSaved, dout):
 TSHIFT_FUSION = int(os.environ.get("SGCN_TSHIFT_FUSION", "1"))
 # fuse only from this many channels up (below, the two-launch form is used)
 TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "128"))
+# Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
+# (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass. A/B knob.
+GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
 
 
 def trainable(module):

@@ -256,6 +256,38 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     return gin, gx, gy
 
 
+GBN_MAX_PLANE = 16384    # sgcn_tshift_bwd_gbn: LDS-staged stride-1 planes only
+
+
+def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats"):
+    """Shift_tcn.shift_in backward (stride 1, Shift_tcn.bn's affine on the taps and its
+    backward partials) that also emits the k-free backward sums of Shift_gcn.bn, whose
+    input is ``z`` and whose ReLU output is ``inp`` (sgcn_tshift_bwd_gbn). Returns
+    (grad_input, grad_xpos, grad_ypos, bn_part, z_part6)."""
+    check_input(gout, "grad_output")
+    check_input(inp, "input")
+    check_input(z, "z")
+    B, C, H, W = inp.shape
+    lib = _lib.load()
+    dev = inp.device
+    gin = torch.empty_like(inp)
+    gx = torch.empty((C,), device=dev, dtype=_F32)
+    gy = torch.empty((C,), device=dev, dtype=_F32)
+    nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
+    ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
+    bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32)
+    zpart = torch.empty((6 * B * C * W,), device=dev, dtype=_F32)
+    nb = 4 * (gout.numel() + 3 * inp.numel())
+    with _timed("tshift_bwd", 0, nb, inp, "GBN " + _shp(inp)):
+        rc = lib.sgcn_tshift_bwd_gbn(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos),
+                                     _ptr(st.scale), _ptr(st.shift), _ptr(st.mean),
+                                     _ptr(st.invstd), _ptr(bpart), _ptr(z), _ptr(zst.mean),
+                                     _ptr(zst.invstd), _ptr(zpart), _ptr(gin), _ptr(gx),
+                                     _ptr(gy), _ptr(ws), nbytes, B, C, H, W, _stream(inp))
+    _lib.check(rc, "sgcn_tshift_bwd_gbn")
+    return gin, gx, gy, bpart, zpart
+
+
 BNIN_MAX_PLANE = 16384   # sgcn_tshift_bwd_bnin: LDS-staged stride-1 planes only
 
 
@@ -553,6 +585,24 @@ def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
                                               _ptr(dgamma), _ptr(dbeta), 0, int(st.batch),
                                               _ptr(coef), _stream(part))
     _lib.check(rc, "sgcn_bn_bwd_finalize")
+    return coef, dgamma, dbeta
+
+
+def bn_bwd_finalize_gbn(part6, B, C, V, n_total, dy_coef, dy_st: BnStats, st: BnStats, bn):
+    """sgcn_bn_bwd_finalize_gbn: the per-joint BatchNorm1d's (coef[3, C*V], dgamma, dbeta)
+    from sgcn_tshift_bwd_gbn's sums and the following BatchNorm's coefficients/mean."""
+    dev = part6.device
+    F = C * V
+    coef = torch.empty((3, F), device=dev, dtype=_F32)
+    dgamma = torch.empty_like(bn.weight) if bn.weight is not None else None
+    dbeta = torch.empty_like(bn.bias) if bn.bias is not None else None
+    with _timed("finalize", 0, 4 * part6.numel(), part6):
+        rc = _lib.load().sgcn_bn_bwd_finalize_gbn(_ptr(part6), B, C, V, int(n_total),
+                                                  _ptr(dy_coef), _ptr(dy_st.mean),
+                                                  _ptr(st.mean), _ptr(st.invstd),
+                                                  _ptr(bn.weight), _ptr(dgamma), _ptr(dbeta), 0,
+                                                  int(st.batch), _ptr(coef), _stream(part6))
+    _lib.check(rc, "sgcn_bn_bwd_finalize_gbn")
     return coef, dgamma, dbeta
 
 

@@ -1,0 +1,122 @@
+"""Shift_gcn.bn's backward partials made by the Shift_tcn.shift_in backward launch
+(sgcn_tshift_bwd_gbn + sgcn_bn_bwd_finalize_gbn; reference model/shift_gcn.py:137-141 then
+:66-68, shift_cuda_kernel.cu:78-150 for the shift backward):
+
+* the shift outputs (input gradient, position gradients, Shift_tcn.bn partials) are
+  bit-identical to sgcn_tshift_bwd's;
+* the per-joint BatchNorm's coefficients and dgamma/dbeta match the two-pass form
+  (sgcn_bn_bwd_reduce with the on-the-fly input gradient + sgcn_bn_bwd_finalize) and an
+  fp64 torch evaluation of the same sums, within 1e-5 relative;
+* unit parity vs the oracle with the fusion off (the default-on path is covered by
+  test_gpu_blocks / test_gpu_fullsize).
+"""
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+CASES = [(4, 64, 30, 25), (2, 128, 17, 25), (3, 32, 9, 33), (2, 16, 300, 25)]
+
+
+def _setup(B, C, T, V, seed):
+    from shiftgcn import ops
+    g = torch.Generator().manual_seed(seed)
+    Z = (torch.randn(B, C, T, V, generator=g) * 2 + 0.5).to(DEV)
+    H = torch.relu(torch.randn(B, C, T, V, generator=g) + 0.3).to(DEV)
+    dAs = torch.randn(B, C, T, V, generator=g).to(DEV)
+    xpos = ((torch.rand(C, generator=g) - 0.5) * 2e-8).to(DEV)
+    ypos = ((torch.rand(C, generator=g) - 0.5) * 4).to(DEV)
+    bn_t, bn_g = nn.BatchNorm2d(C).to(DEV), nn.BatchNorm1d(C * V).to(DEV)
+    with torch.no_grad():
+        bn_t.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn_t.bias.copy_(torch.randn(C, generator=g))
+        bn_g.weight.copy_(torch.rand(C * V, generator=g) + 0.5)
+        bn_g.bias.copy_(torch.randn(C * V, generator=g))
+    ast = ops.bn_finalize(ops.moments(H, False), B, C, T * V, bn_t)
+    zst = ops.bn_finalize(ops.moments(Z, True), B, C * V, T, bn_g, perm_V=V)
+    return Z, H, dAs, xpos, ypos, bn_t, bn_g, ast, zst
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max()) / (float(b.abs().max()) + 1e-30)
+
+
+@pytest.mark.parametrize("case", CASES, ids=["x".join(map(str, c)) for c in CASES])
+def test_gbn_matches_two_pass(case):
+    from shiftgcn import ops
+    B, C, T, V = case
+    Z, H, dAs, xpos, ypos, bn_t, bn_g, ast, zst = _setup(B, C, T, V, sum(case))
+    dA1, gx1, gy1, part1 = ops.tshift_bwd(dAs, H, xpos, ypos, 1, scale=ast.scale,
+                                          shift=ast.shift, bn_stats=ast)
+    dA2, gx2, gy2, part2, z6 = ops.tshift_bwd_gbn(dAs, H, xpos, ypos, ast, Z, zst)
+    torch.cuda.synchronize()
+    assert torch.equal(dA1, dA2) and torch.equal(gx1, gx2) and torch.equal(gy1, gy2)
+    assert torch.equal(part1, part2)
+    coefA, _, _ = ops.bn_bwd_finalize(part1, B, C, B * T * V, ast, bn_t)
+    # two-pass reference: reduce over (dA, H, Z) with the on-the-fly input gradient
+    rp, _ = ops.bn_bwd_reduce(dA1, H, True, Z, zst, True, dy_coef=coefA)
+    c_ref, dg_ref, db_ref = ops.bn_bwd_finalize(rp, B, C * V, B * T, zst, bn_g, perm_V=V)
+    c_new, dg_new, db_new = ops.bn_bwd_finalize_gbn(z6, B, C, V, B * T, coefA, ast, zst, bn_g)
+    # fp64 evaluation of the same sums (reference feature order v*C + c)
+    k = coefA.double()
+    gd = (k[0].view(1, C, 1, 1) * dA1.double() + k[1].view(1, C, 1, 1) * H.double()
+          + k[2].view(1, C, 1, 1)) * (H > 0)
+    zh = (Z.double() - zst.mean.double().view(1, C, 1, V)) * zst.invstd.double().view(1, C, 1, V)
+    sg = gd.sum((0, 2)).t().reshape(-1)                 # (C, V) -> (V, C) -> v*C + c
+    sgx = (gd * zh).sum((0, 2)).t().reshape(-1)
+    torch.cuda.synchronize()
+    assert _rel(db_new, sg) < 1e-5 and _rel(dg_new, sgx) < 1e-5
+    assert _rel(db_new, db_ref) < 1e-5 and _rel(dg_new, dg_ref) < 1e-5
+    assert _rel(c_new[0], c_ref[0]) == 0.0                # k1 = gamma * invstd, same floats
+    assert _rel(c_new[1], c_ref[1]) < 1e-5 and _rel(c_new[2], c_ref[2]) < 1e-5
+
+
+def test_unit_parity_with_gbn_off(monkeypatch):
+    import formula
+    import shiftgcn
+    from oracle import model_oracle as mo
+    from shiftgcn import fused
+    from test_gpu_blocks import _compare
+    monkeypatch.setattr(fused, "GBN_FUSION", 0)
+    ref = mo.TCN_GCN_unit(64, 64, None, stride=1, num_point=25)
+    formula.fill_state(ref, seed=23)
+    ours = shiftgcn.TCN_GCN_unit(64, 64, None, stride=1, num_point=25).to(DEV)
+    ours.load_state_dict(ref.state_dict())
+    x = formula.tensor((3, 64, 14, 25), 71, 1.0)
+    g = formula.tensor((3, 64, 14, 25), 72, 1.0)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(g)
+    xo = x.to(DEV).requires_grad_(True)
+    yo = ours(xo)
+    yo.backward(g.to(DEV))
+    torch.cuda.synchronize()
+    _compare(ref, ours, xr, yr, xo, yo, "gbn-off")
+
+
+def test_gbn_path_taken_in_model(monkeypatch):
+    """Units without a down conv take the fused path: no bn_bwd_reduce on their per-joint
+    BatchNorm (only l1/l5/l8, which have down convs, and the unit-tail reduces remain)."""
+    import shiftgcn
+    from shiftgcn import ops
+    calls = {"gbn": 0, "pj_reduce": 0}
+    real_gbn, real_red = ops.tshift_bwd_gbn, ops.bn_bwd_reduce
+
+    def spy_gbn(*a, **k):
+        calls["gbn"] += 1
+        return real_gbn(*a, **k)
+
+    def spy_red(dy, y, relu, x, st, per_joint, *a, **k):
+        calls["pj_reduce"] += int(bool(per_joint))
+        return real_red(dy, y, relu, x, st, per_joint, *a, **k)
+
+    monkeypatch.setattr(ops, "tshift_bwd_gbn", spy_gbn)
+    monkeypatch.setattr(ops, "bn_bwd_reduce", spy_red)
+    m = shiftgcn.Model(num_class=60, num_point=25, num_person=2,
+                       graph="graph.ntu_rgb_d.Graph").to(DEV).train()
+    m(torch.randn(2, 3, 16, 25, 2, device=DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert calls == {"gbn": 7, "pj_reduce": 3}, calls
