@@ -131,8 +131,8 @@ int sgcn_tshift_bwd_f64(const double* gout, const double* in, const double* xpos
  * z_invstd[c*W+w], mu = bn_mean[c]; z = that BatchNorm's input (the gcn contraction
  * output), statistics in the per-joint local order. Feed z_part to
  * sgcn_bn_bwd_finalize_gbn; no separate sgcn_bn_bwd_reduce pass over (gin, in, z).
- * H*W <= 16384 and W <= 256 only (else SGCN_EINVAL: use sgcn_tshift_bwd +
- * sgcn_bn_bwd_reduce). */
+ * H*W <= 16384, W <= 64 and H*W <= 32 * (512 / W) * W only (else SGCN_EINVAL: use
+ * sgcn_tshift_bwd + sgcn_bn_bwd_reduce). */
 int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
                         const float* ypos, const float* in_scale, const float* in_shift,
                         const float* bn_mean, const float* bn_invstd, float* bn_part,

@@ -569,11 +569,26 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
+  // GBN: elements are dealt to the first NTE = (NT / W) * W threads with stride NTE, so a
+  // thread's joint w = threadIdx.x % W is the same for all its elements and the per-joint
+  // sums accumulate in registers (the remaining NT - NTE threads hold no elements)
+  const int NTE = GBN ? (NT / W) * W : NT;
+  const bool own = !GBN || (int)threadIdx.x < NTE;
+  float zr[GBN ? LPT : 1];
   if (RA) {   // gout -> LDS, own input elements -> registers, all loads in flight together
     const float* __restrict__ go = gout + (size_t)plane * nt;
     const float* __restrict__ src = in + (size_t)plane * nb;
     float t[LPT];
-    if (GP) {
+    if (GBN) {
+      const float* __restrict__ zp = gz + (size_t)plane * nb;
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) {
+        const int i = min(e * NTE + (int)threadIdx.x, nt - 1);
+        t[e] = go[i];
+        rin_r[e] = src[i];
+        zr[e] = zp[i];
+      }
+    } else if (GP) {
       const size_t po = (size_t)plane * nt;
       const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
       float u1[LPT], u2[LPT];
@@ -596,8 +611,8 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     }
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
-      const int i = e * NT + threadIdx.x;
-      if (i < nt) lds[i] = t[e];
+      const int i = e * NTE + threadIdx.x;
+      if (own && i < nt) lds[i] = t[e];
     }
   } else {  // one staging pass: both planes' loads in flight together (LPT covers nt + nb)
     const float* __restrict__ go = gout + (size_t)plane * nt;
@@ -621,15 +636,21 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   // (1) grad_input over the bottom grid (.cu:108-150 stride 1; .cu:191-254 stride 2)
   float bs0 = 0.f, bs1 = 0.f;
   float ax = 0.f, ay = 0.f;
-  float dav[GBN ? LPT : 1];   // GBN: this thread's input gradients, for the joint partials
+  float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // GBN per-joint sums (see the header)
+  float zm = 0.f, zi = 0.f;
+  if (GBN) {
+    const int w = (int)threadIdx.x % W;
+    zm = gzm[c * W + w];
+    zi = gzi[c * W + w];
+  }
   if (RA) {
     const Geom r = make_geom(-x, -y);
     const Geom g = make_geom(x, y);
-    Walker pos(threadIdx.x, NT, W);
+    Walker pos(threadIdx.x, NTE, W);
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
-      const int o = e * NT + threadIdx.x;
-      if (o < nb) {
+      const int o = e * NTE + threadIdx.x;
+      if (own && o < nb) {
         TapIdx ti;
         tap_idx(pos.h + r.y1, pos.w + r.x1, Ho, W, ti);
         const float q11 = sel(gs[ti.o00], ti.m00), q21 = sel(gs[ti.o01], ti.m01);
@@ -638,7 +659,15 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
         const float rin = rin_r[e];
         if (RELU_MASK) val = rin > 0.f ? val : 0.f;
         gi[o] = val;
-        if (GBN) dav[e] = val;
+        if (GBN && rin > 0.f) {
+          const float hc = rin - bmu, zh = (zr[e] - zm) * zi;
+          a6[0] += val;
+          a6[1] += hc;
+          a6[2] += 1.f;
+          a6[3] += val * zh;
+          a6[4] += hc * zh;
+          a6[5] += zh;
+        }
         if (BNP) {
           bs0 += val;
           bs1 += val * ((rin - bmu) * bis);
@@ -720,102 +749,13 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     if (threadIdx.x == 0) bn_part[plane] = make_float2(bs0, bs1);
   }
   if (GBN) {
-    __syncthreads();   // every LDS read of gout is done: the plane's dA goes there instead
-#pragma unroll
-    for (int e = 0; e < LPT; ++e) {
-      const int o = e * NT + threadIdx.x;
-      if (o < nb) lds[o] = dav[e];
-    }
-    __syncthreads();
-    // per joint: thread (v, row group r) walks rows r, r + G, ... (coalesced H/Z rows)
-    const int G = NT / W;
-    float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if ((int)threadIdx.x < G * W) {
-      const int v = threadIdx.x % W, r = threadIdx.x / W;
-      const float zm = gzm[c * W + v], zi = gzi[c * W + v];
-      const float* __restrict__ hp = in + (size_t)plane * nb;
-      const float* __restrict__ zp = gz + (size_t)plane * nb;
-      for (int t0 = r; t0 < Hb; t0 += 4 * G) {
-        float hv[4], zv[4], dv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int o = min(t0 + u * G, Hb - 1) * W + v;
-          hv[u] = hp[o];
-          zv[u] = zp[o];
-          dv[u] = lds[o];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (t0 + u * G < Hb && hv[u] > 0.f) {
-            const float hc = hv[u] - bmu, zh = (zv[u] - zm) * zi;
-            a6[0] += dv[u];
-            a6[1] += hc;
-            a6[2] += 1.f;
-            a6[3] += dv[u] * zh;
-            a6[4] += hc * zh;
-            a6[5] += zh;
-          }
-        }
-      }
-    }
-    __syncthreads();   // dA reads done: the LDS now holds the 6 x NT per-thread sums
+    // merge the G = NTE / W row groups of each joint in fixed order (deterministic)
+    __syncthreads();   // every LDS read of gout is done: reuse the LDS (>= 6*NT floats)
 #pragma unroll
     for (int k = 0; k < 6; ++k) lds[k * NT + threadIdx.x] = a6[k];
     __syncthreads();
     if ((int)threadIdx.x < W) {
-      const size_t np = (size_t)gridDim.x * W;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        float sum = 0.f;
-        for (int g = 0; g < G; ++g) sum += lds[k * NT + g * W + threadIdx.x];
-        gzpart[k * np + (size_t)plane * W + threadIdx.x] = sum;
-      }
-    }
-  }
-  if (GBN) {
-    __syncthreads();   // every LDS read of gout is done: the plane's dA goes there instead
-#pragma unroll
-    for (int e = 0; e < LPT; ++e) {
-      const int o = e * NT + threadIdx.x;
-      if (o < nb) lds[o] = dav[e];
-    }
-    __syncthreads();
-    // per joint: thread (v, row group r) walks rows r, r + G, ... (coalesced H/Z rows)
-    const int G = NT / W;
-    float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if ((int)threadIdx.x < G * W) {
-      const int v = threadIdx.x % W, r = threadIdx.x / W;
-      const float zm = gzm[c * W + v], zi = gzi[c * W + v];
-      const float* __restrict__ hp = in + (size_t)plane * nb;
-      const float* __restrict__ zp = gz + (size_t)plane * nb;
-      for (int t0 = r; t0 < Hb; t0 += 4 * G) {
-        float hv[4], zv[4], dv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int o = min(t0 + u * G, Hb - 1) * W + v;
-          hv[u] = hp[o];
-          zv[u] = zp[o];
-          dv[u] = lds[o];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (t0 + u * G < Hb && hv[u] > 0.f) {
-            const float hc = hv[u] - bmu, zh = (zv[u] - zm) * zi;
-            a6[0] += dv[u];
-            a6[1] += hc;
-            a6[2] += 1.f;
-            a6[3] += dv[u] * zh;
-            a6[4] += hc * zh;
-            a6[5] += zh;
-          }
-        }
-      }
-    }
-    __syncthreads();   // dA reads done: the LDS now holds the 6 x NT per-thread sums
-#pragma unroll
-    for (int k = 0; k < 6; ++k) lds[k * NT + threadIdx.x] = a6[k];
-    __syncthreads();
-    if ((int)threadIdx.x < W) {
+      const int G = NTE / W;
       const size_t np = (size_t)gridDim.x * W;
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
@@ -1134,7 +1074,7 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
                         const float* z, const float* z_mean, const float* z_invstd,
                         float* z_part, float* gin, float* gx, float* gy, void* ws,
                         size_t ws_bytes, int B, int C, int H, int W, void* stream) {
-  SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && W <= 256);
+  SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && W <= 64);
   SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
   SGCN_REQUIRE(gout && in && xpos && ypos && in_scale && in_shift && bn_mean && bn_invstd &&
                bn_part && z && z_mean && z_invstd && z_part && gin && gx && gy && ws);
@@ -1148,11 +1088,18 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
       <<<B * C, NT, (size_t)max(H * W, 6 * NT) * sizeof(float), st>>>(                          \
           gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, C, H, W,   \
           H, 0, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part)
-  // same thread/LPT choice as sgcn_tshift_bwd's stride-1 LDS path
-  if (H * W <= 2048) SGCN_GBN(256, 8);
-  else if (H * W <= 4096) SGCN_GBN(256, 16);
-  else {
-    const int lpt = pick_lpt(H * W, kBwdThreads);
+  // sgcn_tshift_bwd's stride-1 thread counts; elements per thread from the W-aligned
+  // stride (NT / W) * W
+  const int n = H * W;
+  const int nte = n <= 4096 ? (256 / W) * W : (kBwdThreads / W) * W;
+  SGCN_REQUIRE((n + nte - 1) / nte <= 32);   // elements per thread within the largest LPT
+  if (n <= 4096) {
+    const int lpt = pick_lpt(n, (256 / W) * W);
+    if (lpt == 8) SGCN_GBN(256, 8);
+    else if (lpt == 16) SGCN_GBN(256, 16);
+    else SGCN_GBN(256, 32);
+  } else {
+    const int lpt = pick_lpt(n, (kBwdThreads / W) * W);
     if (lpt == 8) SGCN_GBN(kBwdThreads, 8);
     else if (lpt == 16) SGCN_GBN(kBwdThreads, 16);
     else SGCN_GBN(kBwdThreads, 32);

@@ -254,8 +254,8 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
     # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
     # the Shift_gcn BatchNorm that produced H)
-    if (gcn_z is not None and GBN_FUSION and si.stride == 1 and V <= 256 and
-            T * V <= ops.GBN_MAX_PLANE):
+    if (gcn_z is not None and GBN_FUSION and si.stride == 1 and V <= 64 and
+            T * V <= min(ops.GBN_MAX_PLANE, 32 * (512 // V) * V)):
         dA, g["shift_in.xpos"], g["shift_in.ypos"], part, zpart = ops.tshift_bwd_gbn(
             dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0], gcn_z[1])
         out["pre6"] = (zpart, s.ast)

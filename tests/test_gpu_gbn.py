@@ -2,8 +2,8 @@
 (sgcn_tshift_bwd_gbn + sgcn_bn_bwd_finalize_gbn; reference model/shift_gcn.py:137-141 then
 :66-68, shift_cuda_kernel.cu:78-150 for the shift backward):
 
-* the shift outputs (input gradient, position gradients, Shift_tcn.bn partials) are
-  bit-identical to sgcn_tshift_bwd's;
+* the input gradient is bit-identical to sgcn_tshift_bwd's, its plane sums (position
+  gradients, Shift_tcn.bn partials) equal up to summation order;
 * the per-joint BatchNorm's coefficients and dgamma/dbeta match the two-pass form
   (sgcn_bn_bwd_reduce with the on-the-fly input gradient + sgcn_bn_bwd_finalize) and an
   fp64 torch evaluation of the same sums, within 1e-5 relative;
@@ -53,8 +53,12 @@ def test_gbn_matches_two_pass(case):
                                           shift=ast.shift, bn_stats=ast)
     dA2, gx2, gy2, part2, z6 = ops.tshift_bwd_gbn(dAs, H, xpos, ypos, ast, Z, zst)
     torch.cuda.synchronize()
-    assert torch.equal(dA1, dA2) and torch.equal(gx1, gx2) and torch.equal(gy1, gy2)
-    assert torch.equal(part1, part2)
+    # the input gradient is bit-identical; the plane sums (position gradients, Shift_tcn.bn
+    # partials) are the same sums over a joint-aligned thread assignment, so only their
+    # summation order differs (the position gradients keep only the sign of theirs)
+    assert torch.equal(dA1, dA2)
+    assert int((gx1 != gx2).sum() + (gy1 != gy2).sum()) <= 1
+    assert _rel(part2, part1) < 1e-6
     coefA, _, _ = ops.bn_bwd_finalize(part1, B, C, B * T * V, ast, bn_t)
     # two-pass reference: reduce over (dA, H, Z) with the on-the-fly input gradient
     rp, _ = ops.bn_bwd_reduce(dA1, H, True, Z, zst, True, dy_coef=coefA)
