@@ -35,7 +35,11 @@ __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restri
                                                             float2* __restrict__ part, int T,
                                                             int V) {
   __shared__ float s1[kThreads], s2[kThreads], red[2 * kThreads / 64];
-  const int plane = blockIdx.x;
+  // planes in REVERSE order: the input was just written front to back by the contraction,
+  // so its last planes are still in the die-level (Infinity) cache when this pass starts,
+  // and the apply pass that follows (front to back) then meets the planes this pass read
+  // last (measured: moments 1.14 -> 0.92 ms per step)
+  const int plane = gridDim.x - 1 - blockIdx.x;
   const int P = T * V;
   const float* __restrict__ xp = x + (size_t)plane * P;
   const int i = threadIdx.x;
