@@ -33,6 +33,12 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// kReverse note: every shift kernel walks its planes last to first. Its main input was
+// written front to back just before it (the contraction output R, the gcn tail's H, the
+// next unit's input gradient), so the last planes are still in the die-level cache; and
+// the contraction that consumes its output (front to back) then starts on the planes it
+// wrote last.
+
 struct Geom {
   int x1, y1;
   float dx, dy;
@@ -111,7 +117,7 @@ __global__ __launch_bounds__(kThreads) void tshift_fwd_kernel(
     const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
     int Ho, int stride, int add_half) {
   __shared__ float red[2 * kThreads / 64];
-  const int plane = blockIdx.x;
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   const float* __restrict__ src = in + (size_t)plane * Hb * W;
   float* __restrict__ dst = out + (size_t)plane * Ho * W;
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
   __shared__ float red[2 * kThreads / 64];
   float bs0 = 0.f, bs1 = 0.f, bmu = 0.f, bis = 0.f;
   if (BNP) { bmu = bn_mean[blockIdx.x % C]; bis = bn_invstd[blockIdx.x % C]; }
-  const int plane = blockIdx.x;
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   const float* __restrict__ go = gout + (size_t)plane * Ho * W;
   const float* __restrict__ src = in + (size_t)plane * Hb * W;
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
     int Ho, int stride, int add_half) {
   extern __shared__ float pl[];   // Hb*W staged input (affine applied)
   __shared__ float red[2 * NT / 64];
-  const int plane = blockIdx.x;
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   float* __restrict__ dst = out + (size_t)plane * Ho * W;
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];   // shift.py:17-18 (fp32 add)
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pre_kernel(
     int Ho, int stride, int add_half) {
   extern __shared__ float pl[];   // Hb*W staged input
   __shared__ float zs_s[1024], zt_s[1024];
-  const int plane = blockIdx.x;
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   const int nb = Hb * W;
   const size_t ioff = (size_t)plane * nb;
@@ -472,7 +478,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
     int stride, int add_half) {
   extern __shared__ float pl[];   // Hb*W staged input
   __shared__ float gm_s[GOUT ? 1024 : 1];
-  const int plane = blockIdx.x;
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   const size_t ooff = (size_t)plane * Ho * W;
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];
@@ -557,7 +563,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   constexpr bool RA = STRIDE == 1;
   extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input (STRIDE 2 only)]
   __shared__ float red[2 * NT / 64];
-  const int plane = blockIdx.x;
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   const int nb = Hb * W, nt = Ho * W;
   float* gs = lds;
