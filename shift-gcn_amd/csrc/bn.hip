@@ -99,48 +99,46 @@ __device__ __forceinline__ int ref_feature(int f, int perm_V, int F) {
   return v * D + d;  // BatchNorm1d(V*C) feature index of (d, v)  (shift_gcn.py:135-137)
 }
 
-// Per-feature sums over the batch of float2 partials, parallel over b: block = 32
-// features x 32 batch slices; the 32 slice sums are added in fixed order (deterministic).
-// Returns the three double sums (x, y, x*x) in the q == 0 threads. These kernels are
-// latency-bound (a few MB of partials), so every partial of a thread is loaded in ONE
-// round trip for B <= 256 (8 loads in flight per thread).
-constexpr int kFeat = 32, kSlices = 32;
+// Per-feature sums over the batch of float2 partials: ONE WAVE PER FEATURE, the lanes
+// striding the batch (4 partials in flight per lane: one round trip for B <= 256), then a
+// fixed xor tree over the wave in double (deterministic). These kernels are pure latency
+// (a few MB of partials); a wave-level tree replaces the former LDS slice merge (32
+// dependent LDS reads). Every lane returns the three double sums (x, y, x*x).
+constexpr int kFW = 4;   // features (waves) per 256-thread block
+__device__ __forceinline__ double wave_dsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
 __device__ __forceinline__ bool feature_sums(const float2* __restrict__ part, int B, int F,
                                              double& sx, double& sy, double& sxx, int& f) {
-  __shared__ double lx[kSlices][kFeat], ly[kSlices][kFeat], lxx[kSlices][kFeat];
-  const int fl = threadIdx.x % kFeat, q = threadIdx.x / kFeat;
-  f = blockIdx.x * kFeat + fl;
+  const int lane = threadIdx.x & 63;
+  f = blockIdx.x * kFW + (int)(threadIdx.x >> 6);
   const int fc = min(f, F - 1);
   double ax = 0.0, ay = 0.0, axx = 0.0;
-  // 8 independent loads in flight per trip (a dependent load per partial left these
-  // latency-bound at ~8 us per launch); the summation order (b ascending) is unchanged
-  for (int b0 = q; b0 < B; b0 += kSlices * 8) {
-    float2 pv[8];
+  for (int b0 = lane; b0 < B; b0 += 64 * 4) {
+    float2 pv[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = b0 + u * kSlices;
+    for (int u = 0; u < 4; ++u) {
+      const int b = b0 + u * 64;
       pv[u] = b < B ? part[(size_t)b * F + fc] : make_float2(0.f, 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       ax += pv[u].x;
       ay += pv[u].y;
       axx += (double)pv[u].x * pv[u].x;
     }
   }
-  lx[q][fl] = ax;
-  ly[q][fl] = ay;
-  lxx[q][fl] = axx;
-  __syncthreads();
-  if (q != 0 || f >= F) return false;
-  sx = sy = sxx = 0.0;
-  for (int k = 0; k < kSlices; ++k) { sx += lx[k][fl]; sy += ly[k][fl]; sxx += lxx[k][fl]; }
-  return true;
+  sx = wave_dsum(ax);
+  sy = wave_dsum(ay);
+  sxx = wave_dsum(axx);
+  return f < F && lane == 0;
 }
 
 // part layout [B][F] of {mean, M2}, each over n_part elements. Equal counts, so
 // mean = avg(mean_b), M2 = sum M2_b + n_part * sum (mean_b - mean)^2 (double).
-__global__ __launch_bounds__(kFeat * kSlices) void bn_finalize_kernel(
+__global__ __launch_bounds__(64 * kFW) void bn_finalize_kernel(
     const float2* __restrict__ part, int B, int F, int n_part, int perm_V,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
@@ -371,7 +369,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
 
 // dgamma = sum g*xhat, dbeta = sum g; dx = k1*g + k2*x + k3 with
 // k1 = gamma*invstd, k2 = -k1*invstd*mean(g*xhat), k3 = -k1*mean(g) - k2*mean_x
-__global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
+__global__ __launch_bounds__(64 * kFW) void bn_bwd_finalize_kernel(
     const float2* __restrict__ part, int B, int F, double n_total, int perm_V,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
@@ -400,40 +398,32 @@ __global__ __launch_bounds__(kFeat * kSlices) void bn_bwd_finalize_kernel(
 // k = dyc[3][C] (Shift_tcn.bn's backward coefficients) and mu = dym[C] (its batch mean),
 // channel c = f / V. The six sums are merged over b in double (32 features x 16 slices,
 // fixed order), then combined once per feature.
-constexpr int kSl6 = 16;
-__global__ __launch_bounds__(kFeat * kSl6) void bn_bwd_finalize_gbn_kernel(
+__global__ __launch_bounds__(64 * kFW) void bn_bwd_finalize_gbn_kernel(
     const float* __restrict__ part6, int B, int F, int V, double n_total,
     const float* __restrict__ dyc, const float* __restrict__ dym, int C,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
     int accumulate, int batch_stats, float* __restrict__ coef) {
-  __shared__ double l6[6][kSl6][kFeat];
-  const int fl = threadIdx.x % kFeat, q = threadIdx.x / kFeat;
-  const int f = blockIdx.x * kFeat + fl;
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kFW + (int)(threadIdx.x >> 6);
   const int fc = min(f, F - 1);
   const size_t np = (size_t)B * F;
-  double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int b0 = q; b0 < B; b0 += kSl6 * 8) {
+  double s6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int b0 = lane; b0 < B; b0 += 64 * 2) {
+    float pv[6][2];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      float pv[8];
+    for (int j = 0; j < 6; ++j)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = b0 + u * kSl6;
-        pv[u] = b < B ? part6[j * np + (size_t)b * F + fc] : 0.f;
+      for (int u = 0; u < 2; ++u) {
+        const int b = b0 + u * 64;
+        pv[j][u] = b < B ? part6[j * np + (size_t)b * F + fc] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[j] += pv[u];
-    }
+    for (int j = 0; j < 6; ++j) s6[j] += (double)pv[j][0] + (double)pv[j][1];
   }
 #pragma unroll
-  for (int j = 0; j < 6; ++j) l6[j][q][fl] = a[j];
-  __syncthreads();
-  if (q != 0 || f >= F) return;
-  double s6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int k = 0; k < kSl6; ++k)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) s6[j] += l6[j][k][fl];
+  for (int j = 0; j < 6; ++j) s6[j] = wave_dsum(s6[j]);
+  if (f >= F || lane != 0) return;
   const int c = f / V;
   const double k1 = dyc[c], k2 = dyc[C + c], c3 = (double)dyc[2 * C + c] + k2 * (double)dym[c];
   const double sg = k1 * s6[0] + k2 * s6[1] + c3 * s6[2];
@@ -648,30 +638,26 @@ __global__ void mask_prep_kernel(const float* __restrict__ mask, float* __restri
 }
 
 // dmask[u][c] (+)= (sum_b part[b][c][u]) * (1 - tanh(mask)^2); parallel over b
-__global__ __launch_bounds__(kFeat * kSlices) void mask_grad_finalize_kernel(
+__global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_kernel(
     const float* __restrict__ part, const float* __restrict__ mask, int B, int C, int V,
     float* __restrict__ dmask, int accumulate) {
-  __shared__ double ls[kSlices][kFeat];
   const int F = C * V;  // part feature f = c*V + u
-  const int fl = threadIdx.x % kFeat, q = threadIdx.x / kFeat;
-  const int f = blockIdx.x * kFeat + fl;
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kFW + (int)(threadIdx.x >> 6);
   const int fc = min(f, F - 1);
   double a = 0.0;
-  for (int b0 = q; b0 < B; b0 += kSlices * 8) {
-    float pv[8];
+  for (int b0 = lane; b0 < B; b0 += 64 * 4) {
+    float pv[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = b0 + u * kSlices;
+    for (int u = 0; u < 4; ++u) {
+      const int b = b0 + u * 64;
       pv[u] = b < B ? part[(size_t)b * F + fc] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a += pv[u];
+    for (int u = 0; u < 4; ++u) a += pv[u];
   }
-  ls[q][fl] = a;
-  __syncthreads();
-  if (q != 0 || f >= F) return;
-  double s = 0.0;
-  for (int k = 0; k < kSlices; ++k) s += ls[k][fl];
+  const double s = wave_dsum(a);
+  if (f >= F || lane != 0) return;
   const int c = f / V, u = f - c * V;
   const int i = u * C + c;
   const float t = tanhf(mask[i]);
@@ -713,7 +699,7 @@ int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
   SGCN_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
   hipStream_t st = (hipStream_t)stream;
-  bn_finalize_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSlices, 0, st>>>(
+  bn_finalize_kernel<<<(F + kFW - 1) / kFW, 64 * kFW, 0, st>>>(
       (const float2*)part, B, F, n_part, perm_V, gamma, beta, eps, momentum, running_mean,
       running_var, num_batches, mean, invstd, scale, shift);
   SGCN_LAUNCH_CHECK();
@@ -798,7 +784,7 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
                          float* coef, void* stream) {
   SGCN_REQUIRE(part && B > 0 && F > 0 && n_total > 0 && mean && invstd && coef);
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
-  bn_bwd_finalize_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSlices, 0, (hipStream_t)stream>>>(
+  bn_bwd_finalize_kernel<<<(F + kFW - 1) / kFW, 64 * kFW, 0, (hipStream_t)stream>>>(
       (const float2*)part, B, F, (double)n_total, perm_V, mean, invstd, gamma, dgamma, dbeta,
       accumulate, batch_stats, coef);
   SGCN_LAUNCH_CHECK();
@@ -813,7 +799,7 @@ int sgcn_bn_bwd_finalize_gbn(const float* part6, int B, int C, int V, long long 
   SGCN_REQUIRE(part6 && B > 0 && C > 0 && V > 0 && n_total > 0 && dy_coef && dy_mean && mean &&
                invstd && coef);
   const int F = C * V;
-  bn_bwd_finalize_gbn_kernel<<<(F + kFeat - 1) / kFeat, kFeat * kSl6, 0, (hipStream_t)stream>>>(
+  bn_bwd_finalize_gbn_kernel<<<(F + kFW - 1) / kFW, 64 * kFW, 0, (hipStream_t)stream>>>(
       part6, B, F, V, (double)n_total, dy_coef, dy_mean, C, mean, invstd, gamma, dgamma, dbeta,
       accumulate, batch_stats, coef);
   SGCN_LAUNCH_CHECK();
@@ -908,7 +894,7 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
 int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,
                             float* dmask, int accumulate, void* stream) {
   SGCN_REQUIRE(part && mask && dmask && B > 0 && C > 0 && V > 0);
-  mask_grad_finalize_kernel<<<(C * V + kFeat - 1) / kFeat, kFeat * kSlices, 0,
+  mask_grad_finalize_kernel<<<(C * V + kFW - 1) / kFW, 64 * kFW, 0,
                               (hipStream_t)stream>>>(part, mask, B, C, V, dmask, accumulate);
   SGCN_LAUNCH_CHECK();
   return 0;

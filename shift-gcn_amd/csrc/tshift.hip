@@ -777,35 +777,35 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
 // up to rounding), then applyShiftConstraint (.cu:370-395) with its float/double
 // promotions: sqrt(dy*dy) in float (correctly rounded), quotients in float, times the
 // double literals 0.0 / 0.01, stored as float; the dr == 0 branch stores 0.0 / 0.0001.
-__global__ __launch_bounds__(1024) void tshift_pos_finalize_kernel(
+__global__ __launch_bounds__(256) void tshift_pos_finalize_kernel(
     const float2* __restrict__ pgrad, int B, int C, float* __restrict__ gx,
     float* __restrict__ gy) {
-  // 32 channels x 32 batch slices per block (one round trip of 8 loads per thread for
-  // B <= 256); slices added in fixed order
-  __shared__ double lx[32][32], ly[32][32];
-  const int cl = threadIdx.x % 32, q = threadIdx.x / 32;
-  const int c = blockIdx.x * 32 + cl;
+  // one wave per channel, lanes striding the batch (one round trip of 4 loads for
+  // B <= 256), fixed xor tree in double: deterministic
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   const int cc = min(c, C - 1);
   double ax = 0.0, ay = 0.0;
-  for (int b0 = q; b0 < B; b0 += 256) {   // 8 independent loads in flight, same order
-    float2 pv[8];
+  for (int b0 = lane; b0 < B; b0 += 256) {
+    float2 pv[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = b0 + u * 32;
+    for (int u = 0; u < 4; ++u) {
+      const int b = b0 + u * 64;
       pv[u] = b < B ? pgrad[(size_t)b * C + cc] : make_float2(0.f, 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       ax += (double)pv[u].x;
       ay += (double)pv[u].y;
     }
   }
-  lx[q][cl] = ax;
-  ly[q][cl] = ay;
-  __syncthreads();
-  if (q != 0 || c >= C) return;
-  double sx = 0.0, sy = 0.0;
-  for (int k = 0; k < 32; ++k) { sx += lx[k][cl]; sy += ly[k][cl]; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ax += __shfl_xor(ax, o, 64);
+    ay += __shfl_xor(ay, o, 64);
+  }
+  if (c >= C || lane != 0) return;
+  const double sx = ax, sy = ay;
   const float Gx = (float)(sx / (double)B);
   const float Gy = (float)(sy / (double)B);
   const float gy2 = Gy * Gy;
@@ -1067,7 +1067,7 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
   else SGCN_BNIN(512, 32);
 #undef SGCN_BNIN
   SGCN_LAUNCH_CHECK();
-  tshift_pos_finalize_kernel<<<(C + 31) / 32, 1024, 0, st>>>(pg, B, C, gx, gy);
+  tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -1112,7 +1112,7 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   }
 #undef SGCN_GBN
   SGCN_LAUNCH_CHECK();
-  tshift_pos_finalize_kernel<<<(C + 31) / 32, 1024, 0, st>>>(pg, B, C, gx, gy);
+  tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -1143,7 +1143,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
       else
         launch_bwd_lds<16, 1, 256>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st);
       SGCN_LAUNCH_CHECK();
-      tshift_pos_finalize_kernel<<<(C + 31) / 32, 1024, 0, st>>>(pg, B, C, gx, gy);
+      tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
       SGCN_LAUNCH_CHECK();
       return 0;
     }
@@ -1166,7 +1166,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
 #undef SGCN_BWD_EPT
   }
   SGCN_LAUNCH_CHECK();
-  tshift_pos_finalize_kernel<<<(C + 31) / 32, 1024, 0, st>>>(pg, B, C, gx, gy);
+  tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
