@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 15
+#define SGCN_ABI_VERSION 16
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -128,8 +128,9 @@ int sgcn_tshift_bwd_f64(const double* gout, const double* in, const double* xpos
  * k-free backward sums of Shift_gcn.bn (the per-joint BatchNorm1d whose ReLU output is
  * `in`): z_part[j][b*C*W + c*W + w], j = {sum gin, sum (in - mu), sum 1, sum gin*zh,
  * sum (in - mu)*zh, sum zh} over t where in > 0, zh = (z - z_mean[c*W+w]) *
- * z_invstd[c*W+w], mu = bn_mean[c]; z = that BatchNorm's input (the gcn contraction
- * output), statistics in the per-joint local order. Feed z_part to
+ * z_invstd[c*W+w], mu = bn_mean[c]; z = that BatchNorm's input as the gcn contraction
+ * stored it BEFORE its shift_out (per_joint = 3 layout: logical joint w at (w - c) mod W),
+ * statistics in the per-joint local order. Feed z_part to
  * sgcn_bn_bwd_finalize_gbn; no separate sgcn_bn_bwd_reduce pass over (gin, in, z).
  * H*W <= 16384, W <= 64 and H*W <= 32 * (512 / W) * W only (else SGCN_EINVAL: use
  * sgcn_tshift_bwd + sgcn_bn_bwd_reduce). */
@@ -211,6 +212,13 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
  * ------------------------------------------------------------------------------------
  * per_joint = 1: BatchNorm1d(V*C) over (n, t) of a (B, C, T, V) tensor, feature
  * f = c*V + v here, reference feature index v*C + c (pass perm_V = V to finalize);
+ * per_joint = 3: the same BatchNorm1d on the Shift_gcn contraction output stored BEFORE
+ * its shift_out (sgcn_pw_fwd with y_rsign = 0): element (c, t, v) of that tensor is the
+ * logical element (c, t, (v + c) mod V) (shift_gcn.py:114-118,136), so the rotation is
+ * applied by these kernels' addressing instead of by the contraction's stores
+ * (sgcn_moments, sgcn_bn_apply: outputs/residual/coefficients at the logical position;
+ * sgcn_bn_bwd_reduce, sgcn_bn_bwd_apply: x read at the pre-rotation position; the latter
+ * also stores dx there, as per_joint = 2);
  * per_joint = 0: BatchNorm2d, feature = channel. */
 
 /* Bytes of the per-(b, feature) partials written by sgcn_moments / sgcn_bn_bwd_reduce. */

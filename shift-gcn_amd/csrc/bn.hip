@@ -30,10 +30,13 @@ constexpr int kU = 4;  // elements in flight per thread per loop trip (all loads
 // the batch is done in double by bn_finalize_kernel.
 constexpr int kUM = 8;   // loads in flight per thread (a single-input reduction)
 
-template <bool PER_JOINT>
+// ZU (per_joint = 3): x holds the Shift_gcn contraction output BEFORE its shift_out, so
+// its joint v is the logical joint (v + c) mod V (shift_gcn.py:114-118,136: z[w] =
+// y[(w - c) mod V]); the partial goes to the logical feature.
+template <bool PER_JOINT, bool ZU = false>
 __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restrict__ x,
                                                             float2* __restrict__ part, int T,
-                                                            int V) {
+                                                            int V, int C) {
   __shared__ float s1[kThreads], s2[kThreads], red[2 * kThreads / 64];
   // planes in REVERSE order: the input was just written front to back by the contraction,
   // so its last planes are still in the die-level (Infinity) cache when this pass starts,
@@ -68,7 +71,12 @@ __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restri
       float ta = 0.f, tq = 0.f;
       for (int g = 0; g < G; ++g) { ta += s1[g * V + i]; tq += s2[g * V + i]; }
       const float n = (float)T;
-      part[(size_t)plane * V + i] = make_float2(xp[i] + ta / n, tq - ta * ta / n);
+      int w = i;
+      if (ZU) {
+        w = i + (plane % C) % V;
+        w = w >= V ? w - V : w;
+      }
+      part[(size_t)plane * V + w] = make_float2(xp[i] + ta / n, tq - ta * ta / n);
     }
   } else {
     const float k0 = xp[0];
@@ -198,7 +206,10 @@ __global__ void bn_eval_coef_kernel(int F, int perm_V, const float* __restrict__
 // OUTX = 2 instead: also write yg = the NEXT Shift_gcn's gathered, masked input
 // yg[c,t,(v - c) mod V] = y[c,t,v] * gm[((v - c) mod V)*C + c] (what sgcn_gcn_gather would
 // make from y), saving that kernel's read of y.
-template <bool PER_JOINT, int RES, bool RELU, int OUTX>
+// ZU: x is the pre-shift_out contraction output (see moments_kernel): its element (t, v) is
+// the logical element (t, (v + c) mod V), where the coefficients, the residual and every
+// output live.
+template <bool PER_JOINT, int RES, bool RELU, int OUTX, bool ZU = false>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     const float* __restrict__ x, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ r,
@@ -234,28 +245,42 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     if (RELU) a = fmaxf(a, 0.f);
     k0 = a;
   }
+  // ZU: logical joint vl of this thread's current element (in-row logical offset vl - v)
+  int vl = v;
+  if (ZU) {
+    vl = v + rc;
+    vl = vl >= V ? vl - V : vl;
+  }
   for (int base = 0; base < P; base += kThreads * kU) {
     float xv[kU], rv[kU];
+    int vq = v, vlq = vl;   // per-u copies for the residual's logical address
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int oc = min(base + u * kThreads + (int)threadIdx.x, P - 1);
       xv[u] = x[off + oc];
-      if (RES) rv[u] = r[off + oc];
+      if (RES) rv[u] = r[off + (ZU ? min(max(oc - vq + vlq, 0), P - 1) : oc)];
+      if (ZU) {
+        vq += dv;
+        vq = vq >= V ? vq - V : vq;
+        vlq += dv;
+        vlq = vlq >= V ? vlq - V : vlq;
+      }
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int o = base + u * kThreads + threadIdx.x;
+      const int ol = ZU ? o - v + vl : o;
       float a = xv[u];
-      if (PER_JOINT) a = a * sc_s[v] + sh_s[v];
+      if (PER_JOINT) a = a * sc_s[vl] + sh_s[vl];
       else a = a * sc + sh;
       if (RES == 1) a += rv[u];
       if (RES == 2) a += rv[u] * rsc + rsh;
       if (RELU) a = fmaxf(a, 0.f);
-      if (o < P) y[off + o] = a;
+      if (o < P) y[off + ol] = a;
       if (OUT_G) {
-        int u2 = v - rc;
+        int u2 = vl - rc;
         u2 = u2 < 0 ? u2 + V : u2;
-        if (o < P) yg[off + o - v + u2] = a * gm_s[u2];
+        if (o < P) yg[off + ol - vl + u2] = a * gm_s[u2];
       }
       if (OUT_STATS) {
         const float d = o < P ? a - k0 : 0.f;
@@ -264,6 +289,8 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
       }
       v += dv;
       if (v >= V) v -= V;
+      vl += dv;   // (== v when !ZU)
+      if (vl >= V) vl -= V;
     }
   }
   if (OUT_STATS) {
@@ -281,7 +308,9 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
 // DYT: the incoming gradient is itself a BatchNorm input-gradient that was never
 // materialised: dy_eff = k1[c]*dy + k2[c]*y + k3[c] with y the tensor read for the ReLU
 // mask (the unit's gcn output H, input of Shift_tcn.bn).
-template <bool PER_JOINT, bool RELU, bool RESBN, bool DYT>
+// ZU (per-joint only): x is the pre-shift_out contraction output; the logical joint v of
+// this thread's column reads it at (v - c) mod V.
+template <bool PER_JOINT, bool RELU, bool RESBN, bool DYT, bool ZU = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -302,6 +331,12 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const int v = i % V, rr = i / V;
     const int vc = min(v, V - 1);
     const float mu = mean[c * V + vc], is = invstd[c * V + vc];
+    int xd = 0;   // ZU: in-row offset of this column's x element
+    if (ZU) {
+      int vx = v - c % V;
+      vx = vx < 0 ? vx + V : vx;
+      xd = vx - v;
+    }
     if (i < G * V) {
       for (int t0 = rr; t0 < T; t0 += G * kU) {
         float gv[kU], yv[kU], xv[kU], rv[kU];
@@ -310,7 +345,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
           const int o = min(t0 + u * G, T - 1) * V + v;
           gv[u] = dy[off + o];
           if (RELU) yv[u] = y[off + o];
-          xv[u] = x[off + o];
+          xv[u] = x[off + o + xd];
           if (RESBN) rv[u] = r[off + o];
         }
 #pragma unroll
@@ -453,7 +488,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ coef, int F, const float* __restrict__ r,
     const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
     float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V) {
-  constexpr bool PER_JOINT = PJM != 0, GATH = PJM == 2;
+  // PJM 3: as 2, and x is the pre-shift_out contraction output, read at the same gathered
+  // (pre-rotation) index the dx store uses
+  constexpr bool PER_JOINT = PJM != 0, GATH = PJM >= 2, XG = PJM == 3;
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
   const size_t off = (size_t)plane * P;
@@ -482,8 +519,19 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
       const int o = min(base + u * kThreads + (int)threadIdx.x, P - 1);
       gv[u] = dy[off + o];
       if (RELU) yv[u] = y[off + o];
-      xv[u] = x[off + o];
+      if (!XG) xv[u] = x[off + o];
       if (RES == 2) rv[u] = r[off + o];
+    }
+    if (XG) {   // the gathered index of element o (joint v advanced per u as below)
+      int vq = v;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int o = min(base + u * kThreads + (int)threadIdx.x, P - 1);
+        const int w = vq - rc;
+        xv[u] = x[off + min(max(o - vq + (w < 0 ? w + V : w), 0), P - 1)];
+        vq += dv;
+        if (vq >= V) vq -= V;
+      }
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -685,8 +733,12 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
   if (B == 0) return 0;
   SGCN_REQUIRE(x && part && T > 0);
   hipStream_t st = (hipStream_t)stream;
-  if (per_joint) moments_kernel<true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V);
-  else moments_kernel<false><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V);
+  SGCN_REQUIRE(per_joint >= 0 && per_joint <= 3 && per_joint != 2);
+  if (per_joint == 3)
+    moments_kernel<true, true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
+  else if (per_joint)
+    moments_kernel<true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
+  else moments_kernel<false><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -739,7 +791,17 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
       : (y_gathered ? SGCN_APPLY_X(PJ, RS, RL, 2) : SGCN_APPLY_X(PJ, RS, RL, 0)))
 #define SGCN_APPLY_R(PJ, RL) \
   if (res == 0) SGCN_APPLY(PJ, 0, RL); else if (res == 1) SGCN_APPLY(PJ, 1, RL); else SGCN_APPLY(PJ, 2, RL)
-  if (per_joint) { if (relu) { SGCN_APPLY_R(true, true); } else { SGCN_APPLY_R(true, false); } }
+  if (per_joint == 3) {   // the Shift_gcn tail on the pre-shift_out contraction output
+    SGCN_REQUIRE(relu && !y_gathered);
+#define SGCN_APPLY_ZU(RS)                                                                      \
+  (ys ? bn_apply_kernel<true, RS, true, 1, true><<<g, kThreads, 0, st>>>(                      \
+            x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V)          \
+      : bn_apply_kernel<true, RS, true, 0, true><<<g, kThreads, 0, st>>>(                      \
+            x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V))
+    if (res == 0) SGCN_APPLY_ZU(0); else if (res == 1) SGCN_APPLY_ZU(1); else SGCN_APPLY_ZU(2);
+#undef SGCN_APPLY_ZU
+  }
+  else if (per_joint) { if (relu) { SGCN_APPLY_R(true, true); } else { SGCN_APPLY_R(true, false); } }
   else { if (relu) { SGCN_APPLY_R(false, true); } else { SGCN_APPLY_R(false, false); } }
 #undef SGCN_APPLY_R
 #undef SGCN_APPLY
@@ -766,7 +828,18 @@ int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x
            : bn_bwd_reduce_kernel<PJ, RL, RB, false><<<g, kThreads, 0, st>>>(                  \
                  dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
                  (float2*)rpart, C, T, V))
-  if (per_joint) {
+  if (per_joint == 3) {   // x = the pre-shift_out contraction output (see the kernel)
+    SGCN_REQUIRE(relu);
+#define SGCN_RED_ZU(RB)                                                                       \
+  (dy_coef ? bn_bwd_reduce_kernel<true, true, RB, true, true><<<g, kThreads, 0, st>>>(          \
+                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
+                 (float2*)rpart, C, T, V)                                                     \
+           : bn_bwd_reduce_kernel<true, true, RB, false, true><<<g, kThreads, 0, st>>>(         \
+                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
+                 (float2*)rpart, C, T, V))
+    if (rb) SGCN_RED_ZU(true); else SGCN_RED_ZU(false);
+#undef SGCN_RED_ZU
+  } else if (per_joint) {
     if (relu) { if (rb) SGCN_RED(true, true, true); else SGCN_RED(true, true, false); }
     else { if (rb) SGCN_RED(true, false, true); else SGCN_RED(true, false, false); }
   } else {
@@ -815,7 +888,7 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
   SGCN_REQUIRE(dy && x && coef && dx && (y || !relu));
   SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE(!rcoef || (r && dr));
-  SGCN_REQUIRE(per_joint >= 0 && per_joint <= 2);
+  SGCN_REQUIRE(per_joint >= 0 && per_joint <= 3);
   hipStream_t st = (hipStream_t)stream;
   const int res = dr == nullptr ? 0 : (rcoef ? 2 : 1);
   const int F = per_joint ? C * V : C;
@@ -827,7 +900,8 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                  dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V))
 #define SGCN_BA_R(PJ, RL) \
   if (res == 0) SGCN_BA(PJ, RL, 0); else if (res == 1) SGCN_BA(PJ, RL, 1); else SGCN_BA(PJ, RL, 2)
-  if (per_joint == 2) { if (relu) { SGCN_BA_R(2, true); } else { SGCN_BA_R(2, false); } }
+  if (per_joint == 3) { SGCN_REQUIRE(relu); SGCN_BA_R(3, true); }
+  else if (per_joint == 2) { if (relu) { SGCN_BA_R(2, true); } else { SGCN_BA_R(2, false); } }
   else if (per_joint) { if (relu) { SGCN_BA_R(1, true); } else { SGCN_BA_R(1, false); } }
   else { if (relu) { SGCN_BA_R(0, true); } else { SGCN_BA_R(0, false); } }
 #undef SGCN_BA_R

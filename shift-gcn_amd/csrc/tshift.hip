@@ -586,13 +586,19 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ src = in + (size_t)plane * nb;
     float t[LPT];
     if (GBN) {
+      // z is the gcn contraction output BEFORE its shift_out: logical joint w of this
+      // thread sits at (w - c) mod W in its row (constant in-row offset zd)
       const float* __restrict__ zp = gz + (size_t)plane * nb;
+      const int w0 = (int)threadIdx.x % W;
+      int wz = w0 - c % W;
+      wz = wz < 0 ? wz + W : wz;
+      const int zd = wz - w0;
 #pragma unroll
       for (int e = 0; e < LPT; ++e) {
         const int i = min(e * NTE + (int)threadIdx.x, nt - 1);
         t[e] = go[i];
         rin_r[e] = src[i];
-        zr[e] = zp[i];
+        zr[e] = zp[min(max(i + zd, 0), nb - 1)];
       }
     } else if (GP) {
       const size_t po = (size_t)plane * nt;

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # same-box A/B of two builds (tuning only, e.g. tools/ab_lib.sh): another in-tree build of
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
-ABI_VERSION = 15
+ABI_VERSION = 16
 EINVAL = -22
 
 _lib = None

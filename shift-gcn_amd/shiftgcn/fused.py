@@ -47,7 +47,7 @@ def _empty(*shape, like):
 # Shift_gcn
 # ======================================================================================
 class GcnSaved:
-    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
+    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments", "pj")
 
 
 def gcn_forward(mod, x0, training):
@@ -60,9 +60,14 @@ def gcn_forward(mod, x0, training):
         m = ops.mask_prep(mod.Feature_Mask)
         xg = ops.gcn_gather(x0, m)    # shift_in gather * mask, once (reused by the dW)
     Z = _empty(B, Cout, T, V, like=x0)
-    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z, 1, +1), Cout, Cin, T, V)
+    # GCN_ZU: Z is stored BEFORE shift_out (plain contraction stores) and the BatchNorm
+    # kernels apply the joint rotation in their addressing (per_joint = 3); else the
+    # contraction's epilogue stores it rotated (per_joint = 1)
+    pj = 3 if GCN_ZU else 1
+    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z, 1, 0 if GCN_ZU else 1),
+               Cout, Cin, T, V)
     if training:
-        zst = ops.bn_finalize(ops.moments(Z, True), B, Cout * V, T, mod.bn, perm_V=V)
+        zst = ops.bn_finalize(ops.moments(Z, pj), B, Cout * V, T, mod.bn, perm_V=V)
     else:
         zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
     D0 = dst = None
@@ -74,11 +79,12 @@ def gcn_forward(mod, x0, training):
             dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn)
         else:
             dst = ops.bn_eval_coef(bn, Cout)
-        H, hm = ops.bn_apply(Z, zst, True, r=D0, rst=dst, relu=True, out_stats=training)
+        H, hm = ops.bn_apply(Z, zst, pj, r=D0, rst=dst, relu=True, out_stats=training)
     else:
-        H, hm = ops.bn_apply(Z, zst, True, r=x0, relu=True, out_stats=training)
+        H, hm = ops.bn_apply(Z, zst, pj, r=x0, relu=True, out_stats=training)
     s = GcnSaved()
     s.x0, s.xg, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, xg, Z, zst, D0, dst, H, m
+    s.pj = pj
     s.h_moments = hm   # moments of H for Shift_tcn.bn, produced by the same launch
     return H, s
 
@@ -101,10 +107,10 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     else:
         if mod.has_down:
             conv, bnd = mod.down[0], mod.down[1]
-            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, r=s.D0,
+            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, s.pj, r=s.D0,
                                             rst=s.dst, dy_coef=dy_coef)
         else:
-            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, True, dy_coef=dy_coef)
+            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, s.pj, dy_coef=dy_coef)
         coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, Cout * V, B * T,
                                                                    s.zst, mod.bn, perm_V=V)
     dZ = _empty(B, Cout, T, V, like=x0)
@@ -114,11 +120,12 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
         coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
             rpart, B, Cout, B * T * V, s.dst, bnd)
         dD0 = _empty(B, Cout, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ,
-                         dy_coef=dy_coef)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2 if s.pj == 1 else 3, r=s.D0,
+                         rcoef=coefD, dr=dD0, dx=dZ, dy_coef=dy_coef)
     else:
         g_id = _empty(B, Cin, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2, dr=g_id, dx=dZ, dy_coef=dy_coef)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2 if s.pj == 1 else 3, dr=g_id, dx=dZ,
+                         dy_coef=dy_coef)
     # dZ is stored gathered (per_joint=2: shift_out transposed by the store), so the
     # einsum/bias grads and dX read it as a plain plane: G(b,d,n) = dZ[b,d,n]
     dLW = torch.empty_like(mod.Linear_weight)
@@ -368,7 +375,8 @@ def unit_forward(unit, x, training):
 def _gcn_z(unit, s: UnitSaved):
     """(Z, zst) of the unit's Shift_gcn when its BatchNorm's backward sums can come out of
     the shift_in backward launch (no down conv: its BN would need another input)."""
-    return None if unit.gcn1.has_down else (s.gs.Z, s.gs.zst)
+    # (sgcn_tshift_bwd_gbn reads Z in the pre-shift_out layout)
+    return None if unit.gcn1.has_down or s.gs.pj != 3 else (s.gs.Z, s.gs.zst)
 
 
 def unit_backward(unit, s: UnitSaved, dout):
@@ -448,6 +456,9 @@ TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "128"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
 # (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass. A/B knob.
 GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
+# Shift_gcn's shift_out applied by the BatchNorm kernels' addressing (per_joint = 3) instead
+# of by the contraction's rotated epilogue stores. A/B knob.
+GCN_ZU = int(os.environ.get("SGCN_GCN_ZU", "1"))
 
 
 def trainable(module):

@@ -35,7 +35,8 @@ def _setup(B, C, T, V, seed):
         bn_g.weight.copy_(torch.rand(C * V, generator=g) + 0.5)
         bn_g.bias.copy_(torch.randn(C * V, generator=g))
     ast = ops.bn_finalize(ops.moments(H, False), B, C, T * V, bn_t)
-    zst = ops.bn_finalize(ops.moments(Z, True), B, C * V, T, bn_g, perm_V=V)
+    # Z is the gcn contraction output before its shift_out (per_joint = 3 layout)
+    zst = ops.bn_finalize(ops.moments(Z, 3), B, C * V, T, bn_g, perm_V=V)
     return Z, H, dAs, xpos, ypos, bn_t, bn_g, ast, zst
 
 
@@ -61,14 +62,16 @@ def test_gbn_matches_two_pass(case):
     assert _rel(part2, part1) < 1e-6
     coefA, _, _ = ops.bn_bwd_finalize(part1, B, C, B * T * V, ast, bn_t)
     # two-pass reference: reduce over (dA, H, Z) with the on-the-fly input gradient
-    rp, _ = ops.bn_bwd_reduce(dA1, H, True, Z, zst, True, dy_coef=coefA)
+    rp, _ = ops.bn_bwd_reduce(dA1, H, True, Z, zst, 3, dy_coef=coefA)
     c_ref, dg_ref, db_ref = ops.bn_bwd_finalize(rp, B, C * V, B * T, zst, bn_g, perm_V=V)
     c_new, dg_new, db_new = ops.bn_bwd_finalize_gbn(z6, B, C, V, B * T, coefA, ast, zst, bn_g)
     # fp64 evaluation of the same sums (reference feature order v*C + c)
     k = coefA.double()
     gd = (k[0].view(1, C, 1, 1) * dA1.double() + k[1].view(1, C, 1, 1) * H.double()
           + k[2].view(1, C, 1, 1)) * (H > 0)
-    zh = (Z.double() - zst.mean.double().view(1, C, 1, V)) * zst.invstd.double().view(1, C, 1, V)
+    idx = (torch.arange(V, device=DEV)[None, :] - torch.arange(C, device=DEV)[:, None]) % V
+    Zl = Z.gather(3, idx.view(1, C, 1, V).expand(B, C, T, V))      # logical (rotated) Z
+    zh = (Zl.double() - zst.mean.double().view(1, C, 1, V)) * zst.invstd.double().view(1, C, 1, V)
     sg = gd.sum((0, 2)).t().reshape(-1)                 # (C, V) -> (V, C) -> v*C + c
     sgx = (gd * zh).sum((0, 2)).t().reshape(-1)
     torch.cuda.synchronize()
