@@ -77,8 +77,9 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
  * gradient of the BatchNorm that follows the shift inside a TCN_GCN_unit (Shift_tcn.bn2,
  * shift_gcn.py:73,161-162), formed while staging: gout = k1*(y > 0 ? dy : 0) + k2*s + k3
  * with dy/y the unit's output gradient/output, s = bn2's input, coef = [3][C] {k1,k2,k3}
- * from sgcn_bn_bwd_finalize. That gradient tensor is never written. H*W <= 16384 only
- * (else SGCN_EINVAL: use sgcn_bn_bwd_apply + sgcn_tshift_bwd). */
+ * from sgcn_bn_bwd_finalize. That gradient tensor is never written. Same plane limits as
+ * sgcn_tshift_bwd_gbn: H*W <= 16384, W <= 64, <= 32 elements per thread (else
+ * SGCN_EINVAL: use sgcn_bn_bwd_apply + sgcn_tshift_bwd). */
 int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const float* coef,
                          const float* in, const float* xpos, const float* ypos, float* gin,
                          float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
@@ -132,8 +133,9 @@ int sgcn_tshift_bwd_f64(const double* gout, const double* in, const double* xpos
  * stored it BEFORE its shift_out (per_joint = 3 layout: logical joint w at (w - c) mod W),
  * statistics in the per-joint local order. Feed z_part to
  * sgcn_bn_bwd_finalize_gbn; no separate sgcn_bn_bwd_reduce pass over (gin, in, z).
- * H*W <= 16384, W <= 64 and H*W <= 32 * (512 / W) * W only (else SGCN_EINVAL: use
- * sgcn_tshift_bwd + sgcn_bn_bwd_reduce). */
+ * H*W <= 16384, W <= 64 and at most 32 elements per thread of the joint-aligned stride
+ * (NT / W) * W, NT = 256 (H*W <= 4096) or 512 (else SGCN_EINVAL: use sgcn_tshift_bwd +
+ * sgcn_bn_bwd_reduce). */
 int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
                         const float* ypos, const float* in_scale, const float* in_shift,
                         const float* bn_mean, const float* bn_invstd, float* bn_part,

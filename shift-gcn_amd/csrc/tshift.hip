@@ -575,11 +575,12 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
-  // GBN: elements are dealt to the first NTE = (NT / W) * W threads with stride NTE, so a
-  // thread's joint w = threadIdx.x % W is the same for all its elements and the per-joint
-  // sums accumulate in registers (the remaining NT - NTE threads hold no elements)
-  const int NTE = GBN ? (NT / W) * W : NT;
-  const bool own = !GBN || (int)threadIdx.x < NTE;
+  // RA (stride 1): elements are dealt to the first NTE = (NT / W) * W threads with stride
+  // NTE, so a thread's joint w = threadIdx.x % W is the same for all its elements: the
+  // column part of every tap is a per-thread constant, and (GBN) the per-joint sums
+  // accumulate in registers (the remaining NT - NTE threads hold no elements)
+  const int NTE = RA ? (NT / W) * W : NT;   // RA: joint-aligned element stride (W <= NT)
+  const bool own = !RA || (int)threadIdx.x < NTE;
   float zr[GBN ? LPT : 1];
   if (RA) {   // gout -> LDS, own input elements -> registers, all loads in flight together
     const float* __restrict__ go = gout + (size_t)plane * nt;
@@ -606,19 +607,19 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
       float u1[LPT], u2[LPT];
 #pragma unroll
       for (int e = 0; e < LPT; ++e) {
-        const int i = min(e * NT + (int)threadIdx.x, nt - 1);
+        const int i = min(e * NTE + (int)threadIdx.x, nt - 1);
         t[e] = gdy[po + i];
         u1[e] = gy[po + i];
         u2[e] = gx[po + i];
-        rin_r[e] = src[min(e * NT + (int)threadIdx.x, nb - 1)];
+        rin_r[e] = src[min(e * NTE + (int)threadIdx.x, nb - 1)];
       }
 #pragma unroll
       for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
     } else {
 #pragma unroll
       for (int e = 0; e < LPT; ++e) {
-        t[e] = go[min(e * NT + (int)threadIdx.x, nt - 1)];
-        rin_r[e] = src[min(e * NT + (int)threadIdx.x, nb - 1)];
+        t[e] = go[min(e * NTE + (int)threadIdx.x, nt - 1)];
+        rin_r[e] = src[min(e * NTE + (int)threadIdx.x, nb - 1)];
       }
     }
 #pragma unroll
@@ -658,15 +659,38 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   if (RA) {
     const Geom r = make_geom(-x, -y);
     const Geom g = make_geom(x, y);
-    Walker pos(threadIdx.x, NTE, W);
+    // the column part of both tap sets is constant per thread (joint-aligned mapping):
+    // clamped column, in-range mask, and the tap-(0,0) offset relative to the element o;
+    // rows are range-checked per element only when a tap row leaves the plane
+    const int w = (int)threadIdx.x % W, h0 = (int)threadIdx.x / W, GR = NTE / W;
+    const int cr = w + r.x1, cq = w - g.x1 - 1;
+    const bool mr0 = (unsigned)cr < (unsigned)W, mr1 = (unsigned)(cr + 1) < (unsigned)W;
+    const bool mq0 = (unsigned)cq < (unsigned)W, mq1 = (unsigned)(cq + 1) < (unsigned)W;
+    const int kr0 = r.y1 * W - w + min(max(cr, 0), W - 1);
+    const int kr1 = r.y1 * W - w + min(max(cr + 1, 0), W - 1);
+    const int kq0 = (-g.y1 - 1) * W - w + min(max(cq, 0), W - 1);
+    const int kq1 = (-g.y1 - 1) * W - w + min(max(cq + 1, 0), W - 1);
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
       const int o = e * NTE + threadIdx.x;
+      const int h = h0 + e * GR;
       if (own && o < nb) {
-        TapIdx ti;
-        tap_idx(pos.h + r.y1, pos.w + r.x1, Ho, W, ti);
-        const float q11 = sel(gs[ti.o00], ti.m00), q21 = sel(gs[ti.o01], ti.m01);
-        const float q12 = sel(gs[ti.o10], ti.m10), q22 = sel(gs[ti.o11], ti.m11);
+        float q11, q21, q12, q22;
+        const int rr = h + r.y1;
+        if ((unsigned)rr < (unsigned)(Ho - 1)) {   // both tap rows inside the plane
+          const int p0 = o + kr0, p1 = o + kr1;
+          q11 = mr0 ? gs[p0] : 0.f;
+          q21 = mr1 ? gs[p1] : 0.f;
+          q12 = mr0 ? gs[p0 + W] : 0.f;
+          q22 = mr1 ? gs[p1 + W] : 0.f;
+        } else {
+          TapIdx ti;
+          tap_idx(rr, cr, Ho, W, ti);
+          q11 = sel(gs[ti.o00], ti.m00);
+          q21 = sel(gs[ti.o01], ti.m01);
+          q12 = sel(gs[ti.o10], ti.m10);
+          q22 = sel(gs[ti.o11], ti.m11);
+        }
         float val = blend(q11, q21, q12, q22, r.dx, r.dy);
         const float rin = rin_r[e];
         if (RELU_MASK) val = rin > 0.f ? val : 0.f;
@@ -685,17 +709,28 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
           bs1 += val * ((rin - bmu) * bis);
         }
         // gout at i - off_k for the forward taps off_k = (y1 + a, x1 + b)
-        TapIdx tj;
-        tap_idx(pos.h - g.y1 - 1, pos.w - g.x1 - 1, Ho, W, tj);
-        const float G11 = sel(gs[tj.o11], tj.m11), G21 = sel(gs[tj.o10], tj.m10);
-        const float G12 = sel(gs[tj.o01], tj.m01), G22 = sel(gs[tj.o00], tj.m00);
+        float G11, G21, G12, G22;
+        const int rq = h - g.y1 - 1;
+        if ((unsigned)rq < (unsigned)(Ho - 1)) {
+          const int p0 = o + kq0, p1 = o + kq1;
+          G22 = mq0 ? gs[p0] : 0.f;
+          G12 = mq1 ? gs[p1] : 0.f;
+          G21 = mq0 ? gs[p0 + W] : 0.f;
+          G11 = mq1 ? gs[p1 + W] : 0.f;
+        } else {
+          TapIdx tj;
+          tap_idx(rq, cq, Ho, W, tj);
+          G11 = sel(gs[tj.o11], tj.m11);
+          G21 = sel(gs[tj.o10], tj.m10);
+          G12 = sel(gs[tj.o01], tj.m01);
+          G22 = sel(gs[tj.o00], tj.m00);
+        }
         const float cx = (1.f - g.dy) * (G21 - G11) + g.dy * (G22 - G12);
         const float cy = (1.f - g.dx) * (G12 - G11) + g.dx * (G22 - G21);
         const float qa = AFFINE ? rin * a + b : rin;
         ax += qa * cx;
         ay += qa * cy;
       }
-      pos.next();
     }
   } else {
     const Geom r = make_geom(-x, -y);
@@ -921,6 +956,15 @@ int pick_lpt(int n, int nt) {
   return per <= 8 ? 8 : (per <= 16 ? 16 : 32);
 }
 
+// elements per thread of the joint-aligned stride-1 LDS backward kernels (stride
+// (nt / W) * W); 0 = the plane does not fit 32 per thread
+int ra_lpt(int n, int nt, int W) {
+  const int nte = (nt / W) * W;
+  if (nte <= 0 || W > 64) return 0;
+  const int per = (n + nte - 1) / nte;
+  return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+}
+
 int pick_ept(int n) {
   const int per = (n + kThreads - 1) / kThreads;
   return per <= 8 ? 8 : (per <= 16 ? 16 : 32);
@@ -1067,10 +1111,14 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
   tshift_bwd_lds_kernel<NT, L, false, true, 1, false, true><<<B * C, NT, lds, st>>>(           \
       nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, C, H, W, \
       H, 0, dy, y, s, coef)
-  if (H * W <= 2048) SGCN_BNIN(256, 8);
-  else if (H * W <= 4096) SGCN_BNIN(256, 16);
-  else if (H * W <= 8192) SGCN_BNIN(512, 16);
-  else SGCN_BNIN(512, 32);
+  const int ntb = H * W <= 4096 ? 256 : 512;
+  const int lpb = ra_lpt(H * W, ntb, W);
+  SGCN_REQUIRE(lpb > 0);   // W <= 64 and <= 32 elements per thread (caller falls back)
+  if (ntb == 256) {
+    if (lpb == 8) SGCN_BNIN(256, 8); else if (lpb == 16) SGCN_BNIN(256, 16); else SGCN_BNIN(256, 32);
+  } else {
+    if (lpb == 8) SGCN_BNIN(512, 8); else if (lpb == 16) SGCN_BNIN(512, 16); else SGCN_BNIN(512, 32);
+  }
 #undef SGCN_BNIN
   SGCN_LAUNCH_CHECK();
   tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
@@ -1103,15 +1151,14 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   // sgcn_tshift_bwd's stride-1 thread counts; elements per thread from the W-aligned
   // stride (NT / W) * W
   const int n = H * W;
-  const int nte = n <= 4096 ? (256 / W) * W : (kBwdThreads / W) * W;
-  SGCN_REQUIRE((n + nte - 1) / nte <= 32);   // elements per thread within the largest LPT
-  if (n <= 4096) {
-    const int lpt = pick_lpt(n, (256 / W) * W);
+  const int ntg = n <= 4096 ? 256 : kBwdThreads;
+  const int lpt = ra_lpt(n, ntg, W);
+  SGCN_REQUIRE(lpt > 0);   // elements per thread within the largest LPT
+  if (ntg == 256) {
     if (lpt == 8) SGCN_GBN(256, 8);
     else if (lpt == 16) SGCN_GBN(256, 16);
     else SGCN_GBN(256, 32);
   } else {
-    const int lpt = pick_lpt(n, (kBwdThreads / W) * W);
     if (lpt == 8) SGCN_GBN(kBwdThreads, 8);
     else if (lpt == 16) SGCN_GBN(kBwdThreads, 16);
     else SGCN_GBN(kBwdThreads, 32);
@@ -1141,24 +1188,31 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   float2* pg = (float2*)ws;
   float2* bp = (float2*)bn_part;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
-  if ((stride == 1 ? H : H + Ho) * W <= kBwdLdsMax && H > 0) {
-    if (stride == 1 && H * W <= 4096) {
-      // small planes (T = 150 / 75): 256 threads, so fewer lanes idle per workgroup
-      if (H * W <= 2048)
-        launch_bwd_lds<8, 1, 256>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st);
-      else
-        launch_bwd_lds<16, 1, 256>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st);
-      SGCN_LAUNCH_CHECK();
-      tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
-      SGCN_LAUNCH_CHECK();
-      return 0;
+  // stride 1: joint-aligned LDS kernels (W <= 64, <= 32 elements per thread); small planes
+  // (T = 150 / 75) on 256 threads, so fewer lanes idle per workgroup
+  const int nt1 = H * W <= 4096 ? 256 : kBwdThreads;
+  const int lpt1 = stride == 1 && H > 0 && H * W <= kBwdLdsMax ? ra_lpt(H * W, nt1, W) : 0;
+  if (lpt1) {
+#define SGCN_BWD1(L, NTT)                                                                       \
+  launch_bwd_lds<L, 1, NTT>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean,       \
+                            bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st)
+    if (nt1 == 256) {
+      if (lpt1 == 8) SGCN_BWD1(8, 256); else if (lpt1 == 16) SGCN_BWD1(16, 256); else SGCN_BWD1(32, 256);
+    } else {
+      if (lpt1 == 8) SGCN_BWD1(8, kBwdThreads); else if (lpt1 == 16) SGCN_BWD1(16, kBwdThreads);
+      else SGCN_BWD1(32, kBwdThreads);
     }
-    const int lpt = pick_lpt(stride == 1 ? H * W : (H + Ho) * W, kBwdThreads);
+#undef SGCN_BWD1
+    SGCN_LAUNCH_CHECK();
+    tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
+    SGCN_LAUNCH_CHECK();
+    return 0;
+  }
+  if (stride == 2 && (H + Ho) * W <= kBwdLdsMax && H > 0) {
+    const int lpt = pick_lpt((H + Ho) * W, kBwdThreads);
 #define SGCN_BWDL_LPT(L)                                                                      \
-  (stride == 1 ? launch_bwd_lds<L, 1>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,  \
-                                      bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st) \
-               : launch_bwd_lds<L, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,  \
-                                      bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st))
+  launch_bwd_lds<L, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, \
+                       gin, pg, bp, B, C, H, W, Ho, ah, st)
     if (lpt == 8) SGCN_BWDL_LPT(8); else if (lpt == 16) SGCN_BWDL_LPT(16); else SGCN_BWDL_LPT(32);
 #undef SGCN_BWDL_LPT
   } else {

@@ -261,8 +261,7 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
     # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
     # the Shift_gcn BatchNorm that produced H)
-    if (gcn_z is not None and GBN_FUSION and si.stride == 1 and V <= 64 and
-            T * V <= min(ops.GBN_MAX_PLANE, 32 * (512 // V) * V)):
+    if gcn_z is not None and GBN_FUSION and si.stride == 1 and ops.ra_fits(T * V, V):
         dA, g["shift_in.xpos"], g["shift_in.ypos"], part, zpart = ops.tshift_bwd_gbn(
             dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0], gcn_z[1])
         out["pre6"] = (zpart, s.ast)
@@ -396,7 +395,7 @@ def unit_backward(unit, s: UnitSaved, dout):
     coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
         part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
     if (kind != "conv" and unit.tcn1.shift_out.stride == 1 and
-            S.shape[2] * S.shape[3] <= ops.BNIN_MAX_PLANE):
+            ops.ra_fits(S.shape[2] * S.shape[3], S.shape[3])):
         # neither dS nor the identity-residual gradient is written: the shift_out backward
         # forms dS while staging, gcn_dx_finish forms dout*(out > 0)
         fo = {}

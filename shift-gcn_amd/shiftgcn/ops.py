@@ -259,6 +259,15 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
 GBN_MAX_PLANE = 16384    # sgcn_tshift_bwd_gbn: LDS-staged stride-1 planes only
 
 
+def ra_fits(n, V):
+    """Whether a stride-1 plane of n = T*V elements fits the joint-aligned LDS backward
+    kernels (sgcn_tshift_bwd_bnin / _gbn): V <= 64, <= 32 elements per thread."""
+    if V > 64 or n > GBN_MAX_PLANE:
+        return False
+    nt = 256 if n <= 4096 else 512
+    return -(-n // ((nt // V) * V)) <= 32
+
+
 def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats"):
     """Shift_tcn.shift_in backward (stride 1, Shift_tcn.bn's affine on the taps and its
     backward partials) that also emits the k-free backward sums of Shift_gcn.bn, whose

@@ -1,0 +1,17 @@
+# SQ counter passes over the training step (3 passes, each its own process and limit):
+#   gpurun -- 'TAG=sq bash tools/gpu_sq_model.sh'   ->  python tools/bench/sq_summary.py gpurun_out/$TAG
+set -e
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/${TAG:-sq}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
+P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM"
+P3="SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_CYCLES SQ_LEVEL_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT"
+i=0
+for P in "$P1" "$P2" "$P3"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/p$i -o run \
+    -- python3 $ROOT/bench.py --steps 1 --warmup 1 --cpu-baseline 0 --roofline 0 > $OUT/p$i.log 2>&1
+  echo PASS_$i
+done
