@@ -43,6 +43,72 @@ def _empty(*shape, like):
     return torch.empty(shape, device=like.device, dtype=torch.float32)
 
 
+# --------------------------------------------------------------------------------------
+# Off-critical-path launches (weight gradients). In a linked chain of units (Model.forward)
+# the weight/bias gradients of every contraction are needed only by the optimizer, so their
+# contractions (MFMA-bound split-K GEMMs + slab reductions) are enqueued on a SIDE stream and
+# run concurrently with the HBM-bound streaming kernels of the input-gradient chain. The
+# first unit of the chain (whose backward runs last) joins the side stream back into the
+# current stream before returning, so everything after loss.backward() sees finished grads.
+# --------------------------------------------------------------------------------------
+_SIDE = {}
+
+
+def _side_stream(device):
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+class _OffPath:
+    """``with _OffPath(on, *operands):`` enqueue the enclosed launches on the side stream,
+    after everything already enqueued on the current stream. Outputs must be allocated
+    BEFORE entering (current-stream memory, joined later); the operands read on the side
+    stream are marked with ``record_stream`` so the caching allocator does not hand their
+    memory to the current stream while the side stream may still read it."""
+
+    __slots__ = ("on", "tensors", "side", "ctx", "ev")
+
+    def __init__(self, on, *tensors):
+        self.on = bool(on)
+        self.tensors = tensors
+
+    def __enter__(self):
+        if not self.on:
+            return self
+        dev = self.tensors[0].device
+        main = torch.cuda.current_stream(dev)
+        self.side = _side_stream(dev)
+        self.side.wait_stream(main)
+        self.ctx = torch.cuda.stream(self.side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if not self.on:
+            return False
+        self.ctx.__exit__(*exc)
+        for t in self.tensors:
+            if t is not None:
+                t.record_stream(self.side)
+        self.ev = torch.cuda.Event()
+        self.ev.record(self.side)
+        return False
+
+    def wait(self):
+        """Make the current stream wait for the enclosed launches (no-op when off)."""
+        if self.on:
+            torch.cuda.current_stream(self.tensors[0].device).wait_event(self.ev)
+
+
+def join_side(device):
+    """Make the current stream wait for every launch enqueued on the side stream."""
+    s = _SIDE.get(device)
+    if s is not None:
+        torch.cuda.current_stream(device).wait_stream(s)
+
+
 # ======================================================================================
 # Shift_gcn
 # ======================================================================================
@@ -50,9 +116,22 @@ class GcnSaved:
     __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments", "pj")
 
 
-def gcn_forward(mod, x0, training):
+def gcn_forward(mod, x0, training, off=False):
+    """``off``: the down conv branch (contraction + statistics) runs on the side stream,
+    concurrently with the gcn contraction, joined before the apply that reads it."""
     B, Cin, T, V = x0.shape
     Cout = mod.out_channels
+    D0 = dst = None
+    if mod.has_down:
+        conv, bn = mod.down[0], mod.down[1]
+        D0 = _empty(B, Cout, T, V, like=x0)
+        down = _OffPath(off, x0)
+        with down:
+            ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
+            if training:
+                dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn)
+            else:
+                dst = ops.bn_eval_coef(bn, Cout)
     cache = mod.__dict__.pop("_gather_cache", None)
     if cache is not None and cache[0] is x0:
         xg, m = cache[1], cache[2]    # made by the previous unit's tail from its registers
@@ -70,15 +149,8 @@ def gcn_forward(mod, x0, training):
         zst = ops.bn_finalize(ops.moments(Z, pj), B, Cout * V, T, mod.bn, perm_V=V)
     else:
         zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
-    D0 = dst = None
     if mod.has_down:
-        conv, bn = mod.down[0], mod.down[1]
-        D0 = _empty(B, Cout, T, V, like=x0)
-        ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
-        if training:
-            dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn)
-        else:
-            dst = ops.bn_eval_coef(bn, Cout)
+        down.wait()
         H, hm = ops.bn_apply(Z, zst, pj, r=D0, rst=dst, relu=True, out_stats=training)
     else:
         H, hm = ops.bn_apply(Z, zst, pj, r=x0, relu=True, out_stats=training)
@@ -90,12 +162,13 @@ def gcn_forward(mod, x0, training):
 
 
 def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, extra_out=None,
-                 pre6=None):
+                 pre6=None, off=False):
     """Returns (dx0, {param_name: grad}). With ``dy_coef`` ([3, Cout]) the incoming
     gradient is dH = k1*dH_arg + k2*H + k3 (Shift_tcn.bn's input gradient), evaluated
     on the fly by the BN-backward kernels instead of being materialised. ``pre6`` =
     (six-sum partials, Shift_tcn.bn stats) from sgcn_tshift_bwd_gbn: bn's backward
-    partials were made by the shift_in backward launch (no reduce pass here)."""
+    partials were made by the shift_in backward launch (no reduce pass here). ``off``:
+    the weight-gradient launches go to the side stream (see _OffPath)."""
     x0 = s.x0
     B, Cin, T, V = x0.shape
     Cout = mod.out_channels
@@ -130,7 +203,8 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     # einsum/bias grads and dX read it as a plain plane: G(b,d,n) = dZ[b,d,n]
     dLW = torch.empty_like(mod.Linear_weight)
     dLb = torch.empty_like(mod.Linear_bias)
-    ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
+    with _OffPath(off, dZ, s.xg):
+        ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
     g["Linear_weight"], g["Linear_bias"] = dLW, dLb
     dXt = _empty(B, Cin, T, V, like=x0)
     ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
@@ -141,11 +215,15 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
                                                               add2_mask=a2m)
     else:
         dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
-    g["Feature_Mask"] = ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V)
+    dmask = torch.empty_like(mod.Feature_Mask)
+    with _OffPath(off, mpart):
+        ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V, out=dmask)
+    g["Feature_Mask"] = dmask
     if mod.has_down:
         dWd = torch.empty_like(conv.weight)
         dbd = torch.empty_like(conv.bias)
-        ops.pw_dw(PV(dD0), PV(x0), dWd, Cout, Cin, T, V, dbias=dbd)
+        with _OffPath(off, dD0, x0):
+            ops.pw_dw(PV(dD0), PV(x0), dWd, Cout, Cin, T, V, dbias=dbd)
         ops.pw_fwd(conv.weight, True, None, PV(dD0), PV(dx), Cin, Cout, T, V, accumulate=True)
         g["down.0.weight"], g["down.0.bias"] = dWd, dbd
     return dx, g
@@ -232,7 +310,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
 
 
 def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_z=None,
-                      out=None):
+                      out=None, off=False):
     """dS: gradient w.r.t. S (pre-bn2). Returns (dH, grads), or ((dA, coef), grads) with
     ``materialize_dx=False`` (dH = coef[0]*dA + coef[1]*H + coef[2], fused downstream).
     ``gcn_z`` = (Z, zst) of the producing Shift_gcn (no down conv): its BatchNorm's
@@ -252,10 +330,12 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     dWt = torch.empty_like(tl.weight)
     dbt = torch.empty_like(tl.bias)
     if s.As is None:   # fused forward: re-form the shifted operand from H while staging
-        ops.pw_dw_tshift(PV(dRp), PV(H), si.xpos.detach(), si.ypos.detach(), s.ast, dWt, Cout, C,
-                         T, V, dbias=dbt)
+        with _OffPath(off, dRp, H, s.ast.scale):
+            ops.pw_dw_tshift(PV(dRp), PV(H), si.xpos.detach(), si.ypos.detach(), s.ast, dWt,
+                             Cout, C, T, V, dbias=dbt)
     else:
-        ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
+        with _OffPath(off, dRp, s.As):
+            ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
     g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
     dAs = _empty(B, C, T, V, like=H)
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
@@ -301,14 +381,15 @@ def convbn_core_forward(mod, x, training):
     return Rc, rst, s
 
 
-def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate):
+def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate, off=False):
     """Conv weight/bias grads and dx (+)= W^T dRc at the strided rows."""
     B, Cin, T, V = s.x.shape
     conv = mod.conv
     Cout = conv.out_channels
     dW = torch.empty_like(conv.weight)
     db = torch.empty_like(conv.bias)
-    ops.pw_dw(PV(dRc), PV(s.x, mod.stride), dW, Cout, Cin, s.To, V, dbias=db)
+    with _OffPath(off, dRc, s.x):
+        ops.pw_dw(PV(dRc), PV(s.x, mod.stride), dW, Cout, Cin, s.To, V, dbias=db)
     ops.pw_fwd(conv.weight, True, None, PV(dRc), PV(dx, mod.stride), Cin, Cout, s.To, V,
                accumulate=accumulate)
     return {"conv.weight": dW, "conv.bias": db}
@@ -318,7 +399,7 @@ def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate):
 # TCN_GCN_unit
 # ======================================================================================
 class UnitSaved:
-    __slots__ = ("x", "gs", "ts", "rs", "out", "prev")
+    __slots__ = ("x", "gs", "ts", "rs", "out", "prev", "off")
 
 
 def unit_forward(unit, x, training):
@@ -343,14 +424,20 @@ def unit_forward(unit, x, training):
     # unit's gcn_dx_finish, which reads x anyway (see unit_backward)
     prev = unit.__dict__.pop("_prev_tail", None)
     prev = prev[1:] if prev is not None and prev[0] is x else None
-    H, gs = gcn_forward(unit.gcn1, x, training)
-    S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
+    off = ASYNC_DW and bool(unit.__dict__.get("_off_path"))   # linked chains only
+    H, gs = gcn_forward(unit.gcn1, x, training, off=off)
     rs = None
+    if unit.residual_kind == "conv":
+        # the residual conv branch runs on the side stream, concurrently with Shift_tcn
+        res = _OffPath(off, x)
+        with res:
+            Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
+    S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
     # the next unit's Shift_gcn (set by Model.forward_planes for the duration of a call):
     # its gathered, masked input is written by this tail launch too
     gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
     if unit.residual_kind == "conv":
-        Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
+        res.wait()
         out = ops.bn_apply(S, sst, False, r=Rc, rst=rst, relu=True, gather_m=gm)
     elif unit.residual_kind == "identity":
         out = ops.bn_apply(S, sst, False, r=x, relu=True, gather_m=gm)
@@ -368,6 +455,7 @@ def unit_forward(unit, x, training):
         nxt.__dict__["_prev_tail"] = (out, S, sst, unit)
     s = UnitSaved()
     s.x, s.gs, s.ts, s.rs, s.out, s.prev = x, gs, ts, rs, out, prev
+    s.off = off
     return out, s
 
 
@@ -378,7 +466,27 @@ def _gcn_z(unit, s: UnitSaved):
     return None if unit.gcn1.has_down or s.gs.pj != 3 else (s.gs.Z, s.gs.zst)
 
 
+def _off_path_ok(unit, s: UnitSaved):
+    """Weight gradients may run on the side stream only if autograd will take the returned
+    gradient tensors as they are (every .grad is None, so AccumulateGrad stores them
+    without launching anything on the current stream before the join)."""
+    if not s.off:
+        return False
+    for p in unit.parameters():
+        if p.requires_grad and p.grad is not None:
+            return False
+    # join at the end of this backward pass, before backward() returns (the engine runs
+    # final callbacks on the caller's current stream)
+    torch.autograd.Variable._execution_engine.queue_callback(
+        lambda dev=s.x.device: join_side(dev))
+    return True
+
+
 def unit_backward(unit, s: UnitSaved, dout):
+    return _unit_backward(unit, s, dout, _off_path_ok(unit, s))
+
+
+def _unit_backward(unit, s: UnitSaved, dout, off):
     ts = s.ts
     S = ts.S
     B, Cout, To, V = S.shape
@@ -401,13 +509,13 @@ def unit_backward(unit, s: UnitSaved, dout):
         fo = {}
         (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, None, materialize_dx=False,
                                             gpre=(dout, s.out, coef2), gcn_z=_gcn_z(unit, s),
-                                            out=fo)
+                                            out=fo, off=off)
         g.update({"tcn1." + k: v for k, v in gt.items()})
         extra = {}
         dx, gg = gcn_backward(unit.gcn1, s.gs, dA,
                               extra_dx=(dout, s.out) if kind == "identity" else None,
                               dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
-                              extra_out=extra, pre6=fo.get("pre6"))
+                              extra_out=extra, pre6=fo.get("pre6"), off=off)
         if s.prev is not None:
             s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
         g.update({"gcn1." + k: v for k, v in gg.items()})
@@ -427,17 +535,17 @@ def unit_backward(unit, s: UnitSaved, dout):
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, dx=dS)
     fo = {}
     (dA, coefA), gt = tcn_core_backward(unit.tcn1, ts, dS, materialize_dx=False,
-                                        gcn_z=_gcn_z(unit, s), out=fo)
+                                        gcn_z=_gcn_z(unit, s), out=fo, off=off)
     g.update({"tcn1." + k: v for k, v in gt.items()})
     extra = {}
     dx, gg = gcn_backward(unit.gcn1, s.gs, dA, extra_dx=dres if kind == "identity" else None,
                           dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
-                          extra_out=extra, pre6=fo.get("pre6"))
+                          extra_out=extra, pre6=fo.get("pre6"), off=off)
     if s.prev is not None:   # kind != "conv" and no gcn down conv: dx is final here
         s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
     g.update({"gcn1." + k: v for k, v in gg.items()})
     if kind == "conv":
-        gr = convbn_dx_and_dw(unit.residual, s.rs, dres, dx, accumulate=True)
+        gr = convbn_dx_and_dw(unit.residual, s.rs, dres, dx, accumulate=True, off=off)
         g.update({"residual." + k: v for k, v in gr.items()})
     return dx, g
 
@@ -458,6 +566,8 @@ GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
 # Shift_gcn's shift_out applied by the BatchNorm kernels' addressing (per_joint = 3) instead
 # of by the contraction's rotated epilogue stores. A/B knob.
 GCN_ZU = int(os.environ.get("SGCN_GCN_ZU", "1"))
+# weight-gradient contractions of linked units on a side stream (_OffPath). A/B knob.
+ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
 
 
 def trainable(module):

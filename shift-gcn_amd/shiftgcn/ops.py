@@ -667,8 +667,8 @@ def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
     return (dx, part) if prev is None else (dx, part, pp)
 
 
-def mask_grad_finalize(part, mask, B, C, V):
-    dmask = torch.empty_like(mask)
+def mask_grad_finalize(part, mask, B, C, V, out=None):
+    dmask = torch.empty_like(mask) if out is None else out
     with _timed("finalize", 0, 4 * part.numel(), mask):
         rc = _lib.load().sgcn_mask_grad_finalize(_ptr(part), _ptr(mask), B, C, V, _ptr(dmask),
                                                  0, _stream(mask))

@@ -214,15 +214,20 @@ def linked_units(units):
     """Run a chain of TCN_GCN_units with the cross-unit fusions on (what Model.forward
     does for l1..l10): each unit's tail launch also writes the next unit's gathered gcn
     input, and the next unit's backward makes this unit's bn2 backward partials. The links
-    live only for the duration of the block (a unit used alone runs unfused)."""
+    live only for the duration of the block (a unit used alone runs unfused). Linked units
+    also run their weight-gradient contractions on a side stream, joined before
+    ``backward()`` returns (fused._OffPath)."""
     try:
         for u, nxt in zip(units[:-1], units[1:]):
             u.__dict__["_gather_consumer"] = nxt.gcn1
             u.__dict__["_next_unit"] = nxt
+        for u in units:
+            u.__dict__["_off_path"] = True
         yield
     finally:
         for u in units:
             u.__dict__.pop("_gather_consumer", None)
             u.__dict__.pop("_next_unit", None)
+            u.__dict__.pop("_off_path", None)
             u.__dict__.pop("_prev_tail", None)
             u.gcn1.__dict__.pop("_gather_cache", None)
