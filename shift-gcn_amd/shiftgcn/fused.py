@@ -52,12 +52,13 @@ def _empty(*shape, like):
 # current stream before returning, so everything after loss.backward() sees finished grads.
 # --------------------------------------------------------------------------------------
 _SIDE = {}
+SIDE_PRIORITY = int(os.environ.get("SGCN_SIDE_PRIORITY", "0"))
 
 
 def _side_stream(device):
     s = _SIDE.get(device)
     if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device=device)
+        s = _SIDE[device] = torch.cuda.Stream(device=device, priority=SIDE_PRIORITY)
     return s
 
 
@@ -203,11 +204,16 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     # einsum/bias grads and dX read it as a plain plane: G(b,d,n) = dZ[b,d,n]
     dLW = torch.empty_like(mod.Linear_weight)
     dLb = torch.empty_like(mod.Linear_bias)
-    with _OffPath(off, dZ, s.xg):
-        ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
-    g["Linear_weight"], g["Linear_bias"] = dLW, dLb
     dXt = _empty(B, Cin, T, V, like=x0)
+    # on the side stream the weight gradient is enqueued after the dX contraction (it then
+    # overlaps the streaming passes that follow instead of competing for the MFMA pipes)
+    if not (off and DW_AFTER_DX):
+        ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
     ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
+    if off and DW_AFTER_DX:
+        with _OffPath(off, dZ, s.xg):
+            ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
+    g["Linear_weight"], g["Linear_bias"] = dLW, dLb
     a2, a2m = extra_dx if isinstance(extra_dx, tuple) else (extra_dx, None)
     if prev is not None:   # also the previous unit's bn2 backward partials (x0 = its out)
         dx, mpart, extra_out["prev_part"] = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id,
@@ -222,9 +228,9 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     if mod.has_down:
         dWd = torch.empty_like(conv.weight)
         dbd = torch.empty_like(conv.bias)
+        ops.pw_fwd(conv.weight, True, None, PV(dD0), PV(dx), Cin, Cout, T, V, accumulate=True)
         with _OffPath(off, dD0, x0):
             ops.pw_dw(PV(dD0), PV(x0), dWd, Cout, Cin, T, V, dbias=dbd)
-        ops.pw_fwd(conv.weight, True, None, PV(dD0), PV(dx), Cin, Cout, T, V, accumulate=True)
         g["down.0.weight"], g["down.0.bias"] = dWd, dbd
     return dx, g
 
@@ -329,16 +335,23 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     tl = mod.temporal_linear
     dWt = torch.empty_like(tl.weight)
     dbt = torch.empty_like(tl.bias)
-    if s.As is None:   # fused forward: re-form the shifted operand from H while staging
-        with _OffPath(off, dRp, H, s.ast.scale):
-            ops.pw_dw_tshift(PV(dRp), PV(H), si.xpos.detach(), si.ypos.detach(), s.ast, dWt,
-                             Cout, C, T, V, dbias=dbt)
-    else:
-        with _OffPath(off, dRp, s.As):
-            ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
-    g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
+
+    def weight_grad():
+        if s.As is None:   # fused forward: re-form the shifted operand from H while staging
+            with _OffPath(off, dRp, H, s.ast.scale):
+                ops.pw_dw_tshift(PV(dRp), PV(H), si.xpos.detach(), si.ypos.detach(), s.ast,
+                                 dWt, Cout, C, T, V, dbias=dbt)
+        else:
+            with _OffPath(off, dRp, s.As):
+                ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
+
+    if not (off and DW_AFTER_DX):
+        weight_grad()
     dAs = _empty(B, C, T, V, like=H)
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
+    if off and DW_AFTER_DX:
+        weight_grad()   # after the dX contraction (see gcn_backward)
+    g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
     # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
     # the Shift_gcn BatchNorm that produced H)
     if gcn_z is not None and GBN_FUSION and si.stride == 1 and ops.ra_fits(T * V, V):
@@ -388,10 +401,10 @@ def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate, off=False):
     Cout = conv.out_channels
     dW = torch.empty_like(conv.weight)
     db = torch.empty_like(conv.bias)
-    with _OffPath(off, dRc, s.x):
-        ops.pw_dw(PV(dRc), PV(s.x, mod.stride), dW, Cout, Cin, s.To, V, dbias=db)
     ops.pw_fwd(conv.weight, True, None, PV(dRc), PV(dx, mod.stride), Cin, Cout, s.To, V,
                accumulate=accumulate)
+    with _OffPath(off, dRc, s.x):
+        ops.pw_dw(PV(dRc), PV(s.x, mod.stride), dW, Cout, Cin, s.To, V, dbias=db)
     return {"conv.weight": dW, "conv.bias": db}
 
 
@@ -568,6 +581,8 @@ GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
 GCN_ZU = int(os.environ.get("SGCN_GCN_ZU", "1"))
 # weight-gradient contractions of linked units on a side stream (_OffPath). A/B knob.
 ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
+# ... enqueued after the dX contraction of the same operand (A/B knob)
+DW_AFTER_DX = int(os.environ.get("SGCN_DW_AFTER_DX", "1"))
 
 
 def trainable(module):
