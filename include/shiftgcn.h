@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 16
+#define SGCN_ABI_VERSION 17
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -43,6 +43,8 @@ int sgcn_abi_version(void);
  *   (a fused BatchNorm apply); both NULL = identity.
  * plane_stats: optional (B*C) float2 {mean, M2} of each output plane (n = H/stride*W),
  *   consumed by sgcn_bn_finalize(); NULL = not computed.
+ * out == NULL (with plane_stats, planes with H*W <= 16384): statistics only, the shift
+ *   output is not written (the training unit tail re-forms it: sgcn_tshift_fwd_tail).
  * Unlike the reference (at::zeros + kernel), every output element is written exactly
  * once (no memset pass). */
 int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float* ypos,
@@ -60,13 +62,17 @@ int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const flo
                         const float* in_shift, int B, int C, int H, int W, int stride,
                         int ypos_is_raw, void* stream);
 
-/* Inference-mode unit tail fused into Shift_tcn's shift_out forward (shift_gcn.py:72-73,
- * 161-162, BatchNorms in eval mode): out = relu(shift(in)*post_scale[c] + post_shift[c]
+/* Unit tail fused into Shift_tcn's shift_out forward (shift_gcn.py:72-73, 161-162):
+ * out = relu(shift(in)*post_scale[c] + post_shift[c]
  * + res), res = 0 (r NULL), r (identity residual) or r*r_scale[c] + r_shift[c] (residual
  * tcn conv output with its eval BN), r laid out like out. gather_m/out_gathered (both or
  * neither): also out_gathered = sgcn_gcn_gather(out, gather_m) for the next unit. The
- * shifted tensor itself is never written. Planes with H*W <= 16384 only (else
- * SGCN_EINVAL: use sgcn_tshift_fwd + sgcn_bn_apply). */
+ * shifted tensor itself is never written. post_scale/post_shift are bn2's apply
+ * coefficients: eval-mode (sgcn_bn_eval_coef) for inference, or training-mode batch
+ * statistics from sgcn_tshift_fwd(out = NULL, plane_stats) + sgcn_bn_finalize (the
+ * backward then re-forms bn2's input: sgcn_tshift_bwd_bnin with s = NULL,
+ * sgcn_gcn_dx_finish / sgcn_bn_bwd_reduce with the shift positions). Planes with
+ * H*W <= 16384 only (else SGCN_EINVAL: use sgcn_tshift_fwd + sgcn_bn_apply). */
 int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const float* ypos,
                          const float* post_scale, const float* post_shift, const float* r,
                          const float* r_scale, const float* r_shift, const float* gather_m,
@@ -77,7 +83,8 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
  * gradient of the BatchNorm that follows the shift inside a TCN_GCN_unit (Shift_tcn.bn2,
  * shift_gcn.py:73,161-162), formed while staging: gout = k1*(y > 0 ? dy : 0) + k2*s + k3
  * with dy/y the unit's output gradient/output, s = bn2's input, coef = [3][C] {k1,k2,k3}
- * from sgcn_bn_bwd_finalize. That gradient tensor is never written. Same plane limits as
+ * from sgcn_bn_bwd_finalize. That gradient tensor is never written. s == NULL: bn2's
+ * input is shift(in) itself (never stored), re-formed from in's taps. Same plane limits as
  * sgcn_tshift_bwd_gbn: H*W <= 16384, W <= 64, <= 32 elements per thread (else
  * SGCN_EINVAL: use sgcn_bn_bwd_apply + sgcn_tshift_bwd). */
 int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const float* coef,
@@ -260,11 +267,16 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
  * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none).
  * dy_coef (optional, [3][C], requires relu): dy is replaced by k1[c]*dy + k2[c]*y + k3[c],
  * i.e. the input gradient of the following BatchNorm2d (whose input is y), computed on the
- * fly instead of materialised (Shift_tcn.bn's dx feeding Shift_gcn's ReLU/BN backward). */
+ * fly instead of materialised (Shift_tcn.bn's dx feeding Shift_gcn's ReLU/BN backward).
+ * x_xpos/x_ypos (optional, both or neither; per_joint = 0, relu, no r / dy_coef): the
+ * BatchNorm input is the stride-1 temporal shift of `x` with these positions, never
+ * written (a TCN_GCN_unit's bn2 input, see sgcn_tshift_fwd_tail); each element is
+ * re-formed from four taps of x, bit-identical to sgcn_tshift_fwd's output. */
 int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x,
-                       const float* mean, const float* invstd, int per_joint, const float* r,
-                       const float* rmean, const float* rinvstd, const float* dy_coef,
-                       float* part, float* rpart, int B, int C, int T, int V, void* stream);
+                       const float* x_xpos, const float* x_ypos, const float* mean,
+                       const float* invstd, int per_joint, const float* r, const float* rmean,
+                       const float* rinvstd, const float* dy_coef, float* part, float* rpart,
+                       int B, int C, int T, int V, void* stream);
 
 /* dgamma/dbeta (+)= sums (reference feature order); coef[3][F] = {k1, k2, k3} such that
  * dx = k1*g + k2*x + k3: the training-mode BatchNorm input gradient (batch_stats = 1), or
@@ -312,11 +324,15 @@ int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, in
  * g = dx*(x0 > 0), xhat = (prev_s - prev_mean[c])*prev_invstd[c] — so the previous
  * unit's backward skips its reduce pass. add2_mask (optional, needs add1 and add2): add2
  * enters as add2 * (add2_mask > 0) (a unit's identity-residual gradient dout*(out > 0),
- * formed here rather than written by the unit tail's BatchNorm backward). */
+ * formed here rather than written by the unit tail's BatchNorm backward).
+ * prev_s_xpos/prev_s_ypos (optional, both or neither, with prev_part): prev_s is the
+ * INPUT of the previous unit's stride-1 shift_out, whose output (bn2's input) was never
+ * written; each element is re-formed from four taps (as sgcn_bn_bwd_reduce's x_xpos). */
 int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
                        const float* add2, const float* add2_mask, float* dx, float* dmask_part,
-                       const float* prev_s, const float* prev_mean, const float* prev_invstd,
-                       float* prev_part, int B, int C, int T, int V, void* stream);
+                       const float* prev_s, const float* prev_s_xpos, const float* prev_s_ypos,
+                       const float* prev_mean, const float* prev_invstd, float* prev_part, int B,
+                       int C, int T, int V, void* stream);
 
 /* dmask[u][c] (+)= (sum_b dmask_part[b][c][u]) * (1 - tanh(mask[u][c])^2). */
 int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,

@@ -53,6 +53,42 @@ __device__ __forceinline__ void block_sum2(float& a, float& b, float* red) {
   b = sb;
 }
 
+// The stride-1 temporal shift of an H x W plane evaluated at one output position (h, w),
+// from the plane's four taps around (h + y1, w + x1) (shift_cuda_kernel.cu:49-73): tap
+// outside the plane = 0, `x1 = floorf(x), dx = x - x1`, the blend left to right with no
+// contraction — the same operations in the same order as tshift.hip's forward kernels,
+// so the value is bit-identical to the element sgcn_tshift_fwd stores. Used by the
+// kernels that read a shift output which is never written (the training unit tail).
+struct ShiftGeom {
+  int x1, y1;
+  float dx, dy;
+};
+__device__ __forceinline__ ShiftGeom shift_geom(float x, float y) {
+#pragma clang fp contract(off)
+  ShiftGeom g;
+  g.x1 = (int)floorf(x);
+  g.y1 = (int)floorf(y);
+  g.dx = x - (float)g.x1;
+  g.dy = y - (float)g.y1;
+  return g;
+}
+__device__ __forceinline__ float shifted_at(const float* __restrict__ p, const ShiftGeom& g,
+                                            int h, int w, int H, int W) {
+#pragma clang fp contract(off)
+  const int r = h + g.y1, c = w + g.x1;
+  const bool r0 = (unsigned)r < (unsigned)H, r1 = (unsigned)(r + 1) < (unsigned)H;
+  const bool c0 = (unsigned)c < (unsigned)W, c1 = (unsigned)(c + 1) < (unsigned)W;
+  const int rr0 = min(max(r, 0), H - 1) * W, rr1 = min(max(r + 1, 0), H - 1) * W;
+  const int cc0 = min(max(c, 0), W - 1), cc1 = min(max(c + 1, 0), W - 1);
+  float q11 = p[rr0 + cc0], q21 = p[rr0 + cc1], q12 = p[rr1 + cc0], q22 = p[rr1 + cc1];
+  q11 = (r0 && c0) ? q11 : 0.f;
+  q21 = (r0 && c1) ? q21 : 0.f;
+  q12 = (r1 && c0) ? q12 : 0.f;
+  q22 = (r1 && c1) ? q22 : 0.f;
+  const float omdx = 1.f - g.dx, omdy = 1.f - g.dy;
+  return q11 * omdx * omdy + q21 * g.dx * omdy + q12 * omdx * g.dy + q22 * g.dx * g.dy;
+}
+
 // Chan et al. merge of (n, mean, M2) partial statistics, in double.
 struct Moments {
   double n, mean, m2;

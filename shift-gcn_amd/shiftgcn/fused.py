@@ -263,10 +263,12 @@ def gcn_infer_z(mod, x0):
     return Z, zst, x0, None
 
 
-def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
+def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None, s_free=False):
     """bn -> shift_in -> temporal_linear -> ReLU -> shift_out; returns (S, bn2 stats, saved)
     where S is the shift_out output BEFORE bn2. ``h_moments``: per-plane moments of H
-    already produced by the launch that wrote H (else computed here)."""
+    already produced by the launch that wrote H (else computed here). ``s_free``
+    (training): S is not written, only its statistics (S = None; the unit tail and the
+    backward re-form it from R)."""
     src = H if H is not None else pre[0]
     B, C, T, V = src.shape
     Cout = mod.out_channels
@@ -305,7 +307,12 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
         return ops.tshift_fwd_tail(R, so.xpos.detach(), so.ypos.detach(), stride, sst,
                                    r=tail[0], rst=tail[1], gather_m=tail[2])
     stats = _empty(B * Cout * 2, like=src) if training else None
-    S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
+    if s_free:
+        assert training and stride == 1
+        S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats,
+                           store=False)
+    else:
+        S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
     if training:
         sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2)
     else:
@@ -434,7 +441,8 @@ def unit_forward(unit, x, training):
             consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
         return out, None
     # the previous unit's tail (its out is x): its bn2 backward partials are made by this
-    # unit's gcn_dx_finish, which reads x anyway (see unit_backward)
+    # unit's gcn_dx_finish, which reads x anyway (see unit_backward); prev = (bn2 input
+    # operand for ops.gcn_dx_finish, that unit)
     prev = unit.__dict__.pop("_prev_tail", None)
     prev = prev[1:] if prev is not None and prev[0] is x else None
     off = ASYNC_DW and bool(unit.__dict__.get("_off_path"))   # linked chains only
@@ -445,11 +453,25 @@ def unit_forward(unit, x, training):
         res = _OffPath(off, x)
         with res:
             Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
-    S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
+    so = unit.tcn1.shift_out
+    T, V = H.shape[2], H.shape[3]
+    # S-free tail (training, stride-1 shift_out, no residual conv): bn2's input S is never
+    # written; its statistics come from a moments-only shift pass, the tail launch re-forms
+    # it from R (sgcn_tshift_fwd_tail), and the backward kernels re-form it from R's taps
+    s_free = (S_FREE and training and unit.residual_kind != "conv" and so.stride == 1 and
+              T * V <= ops.TAIL_MAX_PLANE and ops.ra_fits(T * V, V))
+    S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments,
+                                  s_free=s_free)
     # the next unit's Shift_gcn (set by Model.forward_planes for the duration of a call):
     # its gathered, masked input is written by this tail launch too
     gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
-    if unit.residual_kind == "conv":
+    if s_free:
+        out = ops.tshift_fwd_tail(ts.R, so.xpos.detach(), so.ypos.detach(), 1, sst,
+                                  r=x if unit.residual_kind == "identity" else None,
+                                  gather_m=gm)
+        if gm is None:
+            out = out[0]
+    elif unit.residual_kind == "conv":
         res.wait()
         out = ops.bn_apply(S, sst, False, r=Rc, rst=rst, relu=True, gather_m=gm)
     elif unit.residual_kind == "identity":
@@ -465,7 +487,9 @@ def unit_forward(unit, x, training):
     # added after) and no gcn down conv (whose dx is accumulated after gcn_dx_finish)
     if (nxt is not None and unit.residual_kind != "conv" and nxt.residual_kind != "conv"
             and not nxt.gcn1.has_down):
-        nxt.__dict__["_prev_tail"] = (out, S, sst, unit)
+        nxt.__dict__["_prev_tail"] = (
+            out, (S, sst) if S is not None else
+            (ts.R, sst, (so.xpos.detach(), so.ypos.detach())), unit)
     s = UnitSaved()
     s.x, s.gs, s.ts, s.rs, s.out, s.prev = x, gs, ts, rs, out, prev
     s.off = off
@@ -502,7 +526,8 @@ def unit_backward(unit, s: UnitSaved, dout):
 def _unit_backward(unit, s: UnitSaved, dout, off):
     ts = s.ts
     S = ts.S
-    B, Cout, To, V = S.shape
+    so = unit.tcn1.shift_out
+    B, Cout, To, V = S.shape if S is not None else ts.R.shape   # S-free: stride 1
     kind = unit.residual_kind
     g = {}
     cached = unit.__dict__.pop("_bwd_part", None)
@@ -511,12 +536,14 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
     elif kind == "conv":
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False, r=s.rs.Rc,
                                         rst=s.rs.rst)
+    elif S is None:   # bn2's input re-formed from R's taps
+        part, rpart = ops.bn_bwd_reduce(dout, s.out, True, ts.R, ts.sst, False,
+                                        x_shift=(so.xpos.detach(), so.ypos.detach()))
     else:
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False)
     coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
         part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
-    if (kind != "conv" and unit.tcn1.shift_out.stride == 1 and
-            ops.ra_fits(S.shape[2] * S.shape[3], S.shape[3])):
+    if kind != "conv" and so.stride == 1 and ops.ra_fits(To * V, V):
         # neither dS nor the identity-residual gradient is written: the shift_out backward
         # forms dS while staging, gcn_dx_finish forms dout*(out > 0)
         fo = {}
@@ -527,12 +554,13 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
         extra = {}
         dx, gg = gcn_backward(unit.gcn1, s.gs, dA,
                               extra_dx=(dout, s.out) if kind == "identity" else None,
-                              dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
+                              dy_coef=coefA, prev=None if s.prev is None else s.prev[0],
                               extra_out=extra, pre6=fo.get("pre6"), off=off)
         if s.prev is not None:
-            s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
+            s.prev[1].__dict__["_bwd_part"] = (dx, extra["prev_part"])
         g.update({"gcn1." + k: v for k, v in gg.items()})
         return dx, g
+    assert S is not None   # S-free units always take the path above
     dS = torch.empty_like(S)
     dres = None
     if kind == "conv":
@@ -552,10 +580,10 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
     g.update({"tcn1." + k: v for k, v in gt.items()})
     extra = {}
     dx, gg = gcn_backward(unit.gcn1, s.gs, dA, extra_dx=dres if kind == "identity" else None,
-                          dy_coef=coefA, prev=None if s.prev is None else s.prev[:2],
+                          dy_coef=coefA, prev=None if s.prev is None else s.prev[0],
                           extra_out=extra, pre6=fo.get("pre6"), off=off)
     if s.prev is not None:   # kind != "conv" and no gcn down conv: dx is final here
-        s.prev[2].__dict__["_bwd_part"] = (dx, extra["prev_part"])
+        s.prev[1].__dict__["_bwd_part"] = (dx, extra["prev_part"])
     g.update({"gcn1." + k: v for k, v in gg.items()})
     if kind == "conv":
         gr = convbn_dx_and_dw(unit.residual, s.rs, dres, dx, accumulate=True, off=off)
@@ -583,6 +611,9 @@ GCN_ZU = int(os.environ.get("SGCN_GCN_ZU", "1"))
 ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
 # ... enqueued after the dX contraction of the same operand (A/B knob)
 DW_AFTER_DX = int(os.environ.get("SGCN_DW_AFTER_DX", "1"))
+# S-free unit tails in training (bn2's input re-formed from R; see unit_forward). A/B knob,
+# off: measured 1.8% slower (measured and rejected).
+S_FREE = int(os.environ.get("SGCN_S_FREE", "0"))
 
 
 def trainable(module):

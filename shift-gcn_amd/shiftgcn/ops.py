@@ -117,11 +117,12 @@ def _opt(t, name):
 # temporal shift
 # --------------------------------------------------------------------------------------
 def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=None,
-               ypos_is_raw=True):
+               ypos_is_raw=True, store=True):
     """Forward shift of ``inp`` (B,C,H,W) -> (B,C,H//stride,W). ``ypos`` is the RAW
     parameter (the +0.5 for stride != 1 is applied in-kernel). Optional fused
     per-channel input affine (scale, shift) and per-plane output moments ``stats``
-    (B*C*2 floats). float64 tensors run the double-precision kernel (no fused options)."""
+    (B*C*2 floats). ``store=False`` (with ``stats``): only the moments, nothing written,
+    returns None. float64 tensors run the double-precision kernel (no fused options)."""
     if inp.dtype == torch.float64:
         if scale is not None or shift is not None or stats is not None:
             raise RuntimeError("the fused shift options are float32-only")
@@ -131,10 +132,13 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
     check_input(ypos, "ypos")
     _opt(scale, "scale"), _opt(shift, "shift"), _opt(stats, "stats")
     B, C, H, W = inp.shape
-    if out is None:
+    if not store:
+        if stats is None or out is not None:
+            raise ValueError("tshift_fwd(store=False) computes the output moments only")
+    elif out is None:
         out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
     lib = _lib.load()
-    nb = 4 * (inp.numel() + out.numel())
+    nb = 4 * (inp.numel() + (out.numel() if store else 0))
     with _timed("tshift_fwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_fwd(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(scale),
                                  _ptr(shift), _ptr(stats), B, C, H, W, stride,
@@ -201,8 +205,10 @@ def tshift_fwd_pre(z, xpos, ypos, stride, zst, r, rst, ast):
 
 
 def tshift_fwd_tail(inp, xpos, ypos, stride, st, r=None, rst=None, gather_m=None):
-    """Inference unit tail: relu(BN_eval(shift(inp)) + res) in one launch (+ the next
-    unit's gathered gcn input when ``gather_m`` is given). Returns (out, gathered|None)."""
+    """Unit tail: relu(BN(shift(inp)) + res) in one launch with the coefficients of ``st``
+    (eval: running statistics; training: the batch statistics of shift(inp) from
+    tshift_fwd(store=False)), + the next unit's gathered gcn input when ``gather_m`` is
+    given. Returns (out, gathered|None)."""
     check_input(inp, "input")
     if r is not None:
         check_input(r, "residual")
@@ -303,7 +309,8 @@ BNIN_MAX_PLANE = 16384   # sgcn_tshift_bwd_bnin: LDS-staged stride-1 planes only
 def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos):
     """Stride-1 shift backward (ReLU mask on ``inp``) whose output gradient is the input
     gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3, formed in the
-    kernel. Returns (grad_input, grad_xpos, grad_ypos)."""
+    kernel (``s`` None: s = shift(inp), re-formed from its taps). Returns (grad_input,
+    grad_xpos, grad_ypos)."""
     B, C, H, W = inp.shape
     lib = _lib.load()
     dev = inp.device
@@ -312,7 +319,8 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos):
     gy = torch.empty((C,), device=dev, dtype=_F32)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
-    with _timed("tshift_bwd", 0, 4 * (3 * dy.numel() + 2 * inp.numel()), inp, _shp(inp)):
+    nb = 4 * ((2 + (s is not None)) * dy.numel() + 2 * inp.numel())
+    with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_bwd_bnin(_ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp),
                                       _ptr(xpos), _ptr(ypos), _ptr(gin), _ptr(gx), _ptr(gy),
                                       _ptr(ws), nbytes, B, C, H, W, 1, _stream(inp))
@@ -565,16 +573,20 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
 
 
 def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats = None,
-                  dy_coef=None):
+                  dy_coef=None, x_shift=None):
+    """``x_shift`` = (xpos, ypos): the BatchNorm input is the stride-1 temporal shift of
+    ``x`` with these positions (never written), re-formed per element."""
     check_input(dy, "grad_output")
     B, C, T, V = x.shape
+    xsx, xsy = x_shift if x_shift is not None else (None, None)
     dev = x.device
     part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=dev, dtype=_F32)
     rpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if r is not None else None
     nb = 4 * x.numel() * (2 + (y is not None) + (r is not None))
     with _timed("bn_bwd_reduce", 0, nb, x, _shp(x)):
-        rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x),
-                                            _ptr(st.mean), _ptr(st.invstd), int(per_joint),
+        rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(xsx),
+                                            _ptr(xsy), _ptr(st.mean), _ptr(st.invstd),
+                                            int(per_joint),
                                             _ptr(r), _ptr(rst.mean) if rst else None,
                                             _ptr(rst.invstd) if rst else None, _ptr(dy_coef),
                                             _ptr(part), _ptr(rpart), B, C, T, V, _stream(x))
@@ -650,17 +662,20 @@ def gcn_gather(x0, m):
 
 def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
     """Returns (dx, dmask partials[, prev_part]); ``prev`` = (S, BnStats) of the previous
-    unit's bn2 adds its backward-reduce partials (see sgcn_gcn_dx_finish)."""
+    unit's bn2 adds its backward-reduce partials (see sgcn_gcn_dx_finish), or
+    (R, BnStats, (xpos, ypos)) when bn2's input S = shift(R) was never written."""
     B, C, T, V = dxt.shape
     dx = torch.empty_like(dxt)
     part = torch.empty((B * C * V,), device=dxt.device, dtype=_F32)
     pp = torch.empty((B * C * 2,), device=dxt.device, dtype=_F32) if prev is not None else None
-    ps, pst = prev if prev is not None else (None, None)
+    ps, pst = prev[:2] if prev is not None else (None, None)
+    psx, psy = prev[2] if prev is not None and len(prev) > 2 else (None, None)
     nb = 4 * dxt.numel() * (3 + sum(t is not None for t in (add1, add2, add2_mask, ps)))
     with _timed("gcn_dx_finish", 0, nb, dxt, _shp(dxt)):
         rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1),
                                             _ptr(add2), _ptr(add2_mask), _ptr(dx), _ptr(part),
-                                            _ptr(ps), _ptr(pst.mean) if pst else None,
+                                            _ptr(ps), _ptr(psx), _ptr(psy),
+                                            _ptr(pst.mean) if pst else None,
                                             _ptr(pst.invstd) if pst else None, _ptr(pp), B, C,
                                             T, V, _stream(dxt))
     _lib.check(rc, "sgcn_gcn_dx_finish")
