@@ -445,7 +445,10 @@ def unit_forward(unit, x, training):
     # operand for ops.gcn_dx_finish, that unit)
     prev = unit.__dict__.pop("_prev_tail", None)
     prev = prev[1:] if prev is not None and prev[0] is x else None
-    off = ASYNC_DW and bool(unit.__dict__.get("_off_path"))   # linked chains only
+    # linked chains only; not while a hipGraph is being captured (the graph replays one
+    # stream's launches in order)
+    off = (ASYNC_DW and bool(unit.__dict__.get("_off_path")) and
+           not torch.cuda.is_current_stream_capturing())
     H, gs = gcn_forward(unit.gcn1, x, training, off=off)
     rs = None
     if unit.residual_kind == "conv":
@@ -507,7 +510,7 @@ def _off_path_ok(unit, s: UnitSaved):
     """Weight gradients may run on the side stream only if autograd will take the returned
     gradient tensors as they are (every .grad is None, so AccumulateGrad stores them
     without launching anything on the current stream before the join)."""
-    if not s.off:
+    if not s.off or torch.cuda.is_current_stream_capturing():
         return False
     for p in unit.parameters():
         if p.requires_grad and p.grad is not None:
