@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 17
+#define SGCN_ABI_VERSION 18
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). */
 int sgcn_abi_version(void);
@@ -95,6 +95,13 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
 /* Workspace bytes for sgcn_tshift_bwd (B*C float2 plane partials). */
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
 
+/* The position-gradient step of sgcn_tshift_bwd / _bnin / _gbn on its own: gx, gy from the
+ * per-plane partials those calls leave in `ws` (mean over the batch, then
+ * applyShiftConstraint, .cu:370-395, 501-509). Those calls skip this step when given
+ * gx = gy = NULL, so it can run later / on another stream (the positions' gradients are
+ * needed only by the optimizer); ws must then stay untouched until it has run. */
+int sgcn_tshift_pos_finalize(const void* ws, int B, int C, float* gx, float* gy, void* stream);
+
 /* Backward of the temporal shift. Replaces
  * `shift_cuda.backward(grad_output, input, output, xpos, ypos, stride)`
  *   (shift_cuda.cpp:25-42 -> shift_cuda_kernel.cu:433-523).
@@ -102,6 +109,7 @@ size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
  * ypos_is_raw as in the forward (the reference passes the saved shifted ypos, raw = 0).
  * gin : (B, C, H, W) input gradient (reference Shift_Bottom_Backward*, .cu:78-256);
  * gx, gy: (C) position gradients = mean over batch of the summed position products
+ *   (both NULL: not computed here; the partials stay in ws for sgcn_tshift_pos_finalize)
  *   (.cu:277-363, 501-509) after applyShiftConstraint (.cu:370-395).
  * in_scale/in_shift: same optional affine as the forward (the position products then
  *   use the affine taps). relu_mask != 0: gin[p] = 0 where in[p] <= 0 (fused ReLU

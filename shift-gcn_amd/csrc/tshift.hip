@@ -1123,7 +1123,7 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
                          int W, int ypos_is_raw, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0);
   SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
-  SGCN_REQUIRE(dy && y && coef && in && xpos && ypos && gin && gx && gy && ws);
+  SGCN_REQUIRE(dy && y && coef && in && xpos && ypos && gin && ws && (gx == nullptr) == (gy == nullptr));
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
   SGCN_REQUIRE((long long)B * C < (1LL << 31));
   (void)ypos_is_raw;   // stride 1: the +0.5 of shift.py:17-18 never applies
@@ -1152,12 +1152,20 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
   }
 #undef SGCN_BNIN
   SGCN_LAUNCH_CHECK();
-  tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
+  if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
 
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C) { return (size_t)B * C * sizeof(float2); }
+
+int sgcn_tshift_pos_finalize(const void* ws, int B, int C, float* gx, float* gy, void* stream) {
+  SGCN_REQUIRE(B > 0 && C > 0 && ws && gx && gy);
+  tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, (hipStream_t)stream>>>((const float2*)ws, B,
+                                                                           C, gx, gy);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
 
 int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
                         const float* ypos, const float* in_scale, const float* in_shift,
@@ -1168,7 +1176,8 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && W <= 64);
   SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
   SGCN_REQUIRE(gout && in && xpos && ypos && in_scale && in_shift && bn_mean && bn_invstd &&
-               bn_part && z && z_mean && z_invstd && z_part && gin && gx && gy && ws);
+               bn_part && z && z_mean && z_invstd && z_part && gin && ws);
+  SGCN_REQUIRE((gx == nullptr) == (gy == nullptr));
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
   SGCN_REQUIRE((long long)B * C < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
@@ -1196,7 +1205,7 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   }
 #undef SGCN_GBN
   SGCN_LAUNCH_CHECK();
-  tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
+  if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
@@ -1210,7 +1219,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
   const int Ho = H / stride;
   SGCN_REQUIRE((gout || Ho == 0) && (in || H == 0) && (gin || H == 0));
-  SGCN_REQUIRE(xpos && ypos && gx && gy && ws);
+  SGCN_REQUIRE(xpos && ypos && ws && (gx == nullptr) == (gy == nullptr));
   SGCN_REQUIRE(!bn_part || (bn_mean && bn_invstd));
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
   SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
@@ -1235,7 +1244,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
     }
 #undef SGCN_BWD1
     SGCN_LAUNCH_CHECK();
-    tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
+    if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
     SGCN_LAUNCH_CHECK();
     return 0;
   }
@@ -1257,7 +1266,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
 #undef SGCN_BWD_EPT
   }
   SGCN_LAUNCH_CHECK();
-  tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
+  if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

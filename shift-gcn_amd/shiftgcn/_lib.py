@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # same-box A/B of two builds (tuning only, e.g. tools/ab_lib.sh): another in-tree build of
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
-ABI_VERSION = 17
+ABI_VERSION = 18
 EINVAL = -22
 
 _lib = None
@@ -37,6 +37,7 @@ SIGNATURES = {
     "sgcn_tshift_fwd_tail": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
                                   _I, _I, _P]),
     "sgcn_tshift_bwd_ws_bytes": (_Z, [_I, _I]),
+    "sgcn_tshift_pos_finalize": (_I, [_P, _I, _I, _P, _P, _P]),
     "sgcn_tshift_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _Z, _I,
                              _I, _I, _I, _I, _I, _P]),
     "sgcn_tshift_fwd_f64": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),

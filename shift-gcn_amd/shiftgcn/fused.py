@@ -103,6 +103,20 @@ class _OffPath:
             torch.cuda.current_stream(self.tensors[0].device).wait_event(self.ev)
 
 
+def _pos_grads(gx, gy, shift):
+    """A shift backward's (grad_xpos, grad_ypos): as returned, or, when its partials were
+    left for later (ops.PosPartials), finalized on the side stream into gradient tensors
+    allocated here."""
+    if not isinstance(gx, ops.PosPartials):
+        return gx, gy
+    if not OFF_SMALL:
+        return gx.finalize(torch.empty_like(shift.xpos), torch.empty_like(shift.ypos))
+    ox, oy = torch.empty_like(shift.xpos), torch.empty_like(shift.ypos)
+    with _OffPath(True, gx.ws):
+        gx.finalize(ox, oy)
+    return ox, oy
+
+
 def join_side(device):
     """Make the current stream wait for every launch enqueued on the side stream."""
     s = _SIDE.get(device)
@@ -333,12 +347,15 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     Cout = mod.out_channels
     si, so = mod.shift_in, mod.shift_out
     g = {}
+    # (off: each shift backward leaves its position-gradient partials for a finalize on the
+    # side stream, _pos_grads: the positions' gradients only feed the optimizer)
     if gpre is not None:   # dS = bn2's input gradient, formed inside the shift backward
-        dRp, g["shift_out.xpos"], g["shift_out.ypos"] = ops.tshift_bwd_bnin(
-            gpre[0], gpre[1], s.S, gpre[2], s.R, so.xpos.detach(), so.ypos.detach())
+        dRp, gx, gy = ops.tshift_bwd_bnin(gpre[0], gpre[1], s.S, gpre[2], s.R,
+                                          so.xpos.detach(), so.ypos.detach(), defer_pos=off)
     else:
-        dRp, g["shift_out.xpos"], g["shift_out.ypos"] = ops.tshift_bwd(
-            dS, s.R, so.xpos.detach(), so.ypos.detach(), so.stride, relu_mask=True)
+        dRp, gx, gy = ops.tshift_bwd(dS, s.R, so.xpos.detach(), so.ypos.detach(), so.stride,
+                                     relu_mask=True, defer_pos=off)
+    g["shift_out.xpos"], g["shift_out.ypos"] = _pos_grads(gx, gy, so)
     tl = mod.temporal_linear
     dWt = torch.empty_like(tl.weight)
     dbt = torch.empty_like(tl.bias)
@@ -362,13 +379,15 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
     # the Shift_gcn BatchNorm that produced H)
     if gcn_z is not None and GBN_FUSION and si.stride == 1 and ops.ra_fits(T * V, V):
-        dA, g["shift_in.xpos"], g["shift_in.ypos"], part, zpart = ops.tshift_bwd_gbn(
-            dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0], gcn_z[1])
+        dA, gx, gy, part, zpart = ops.tshift_bwd_gbn(
+            dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0], gcn_z[1],
+            defer_pos=off)
         out["pre6"] = (zpart, s.ast)
     else:
-        dA, g["shift_in.xpos"], g["shift_in.ypos"], part = ops.tshift_bwd(
+        dA, gx, gy, part = ops.tshift_bwd(
             dAs, H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=s.ast.scale,
-            shift=s.ast.shift, bn_stats=s.ast)
+            shift=s.ast.shift, bn_stats=s.ast, defer_pos=off)
+    g["shift_in.xpos"], g["shift_in.ypos"] = _pos_grads(gx, gy, si)
     coef, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, C, B * T * V, s.ast,
                                                              mod.bn)
     if not materialize_dx:
@@ -449,6 +468,13 @@ def unit_forward(unit, x, training):
     # stream's launches in order)
     off = (ASYNC_DW and bool(unit.__dict__.get("_off_path")) and
            not torch.cuda.is_current_stream_capturing())
+    # the next unit's gcn mask (tanh(Feature_Mask) + 1), needed by this unit's tail launch:
+    # a tiny kernel, made on the side stream off the critical path
+    mp = None
+    if consumer is not None:
+        mp = _OffPath(off and OFF_SMALL, consumer.Feature_Mask)
+        with mp:
+            gm = ops.mask_prep(consumer.Feature_Mask)
     H, gs = gcn_forward(unit.gcn1, x, training, off=off)
     rs = None
     if unit.residual_kind == "conv":
@@ -467,7 +493,10 @@ def unit_forward(unit, x, training):
                                   s_free=s_free)
     # the next unit's Shift_gcn (set by Model.forward_planes for the duration of a call):
     # its gathered, masked input is written by this tail launch too
-    gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
+    if mp is not None:
+        mp.wait()
+    else:
+        gm = None
     if s_free:
         out = ops.tshift_fwd_tail(ts.R, so.xpos.detach(), so.ypos.detach(), 1, sst,
                                   r=x if unit.residual_kind == "identity" else None,
@@ -612,6 +641,8 @@ GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
 GCN_ZU = int(os.environ.get("SGCN_GCN_ZU", "1"))
 # weight-gradient contractions of linked units on a side stream (_OffPath). A/B knob.
 ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
+# ... with the small off-path kernels too (position-gradient finalize, next unit's mask)
+OFF_SMALL = int(os.environ.get("SGCN_OFF_SMALL", "1"))
 # ... enqueued after the dX contraction of the same operand (A/B knob)
 DW_AFTER_DX = int(os.environ.get("SGCN_DW_AFTER_DX", "1"))
 # S-free unit tails in training (bn2's input re-formed from R; see unit_forward). A/B knob,

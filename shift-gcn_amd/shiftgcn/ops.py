@@ -225,10 +225,39 @@ def tshift_fwd_tail(inp, xpos, ypos, stride, st, r=None, rst=None, gather_m=None
     return out, og
 
 
+class PosPartials:
+    """Per-plane position-gradient partials left by a shift backward called with
+    ``defer_pos=True``; ``finalize(gx, gy)`` runs sgcn_tshift_pos_finalize on the current
+    stream (e.g. a side stream: the positions' gradients only feed the optimizer)."""
+
+    __slots__ = ("ws", "B", "C")
+
+    def __init__(self, ws, B, C):
+        self.ws, self.B, self.C = ws, B, C
+
+    def finalize(self, gx, gy):
+        check_input(gx, "gx")
+        check_input(gy, "gy")
+        with _timed("finalize", 0, self.ws.numel() * 4, self.ws):
+            rc = _lib.load().sgcn_tshift_pos_finalize(_ptr(self.ws), self.B, self.C, _ptr(gx),
+                                                      _ptr(gy), _stream(self.ws))
+        _lib.check(rc, "sgcn_tshift_pos_finalize")
+        return gx, gy
+
+
+def _pos_out(defer_pos, ws, B, C, dev):
+    """(gx, gy) tensors for the kernel, or (None, None) + PosPartials when deferred."""
+    if defer_pos:
+        return None, None, PosPartials(ws, B, C)
+    return (torch.empty((C,), device=dev, dtype=_F32), torch.empty((C,), device=dev, dtype=_F32),
+            None)
+
+
 def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=False,
-               ypos_is_raw=True, bn_stats=None):
+               ypos_is_raw=True, bn_stats=None, defer_pos=False):
     """Backward shift: returns (grad_input, grad_xpos, grad_ypos), plus the BatchNorm
     backward partials of ``bn_stats`` (the BN whose output feeds the shift) if given.
+    ``defer_pos``: grad_xpos is a PosPartials and grad_ypos None (see PosPartials).
     float64 tensors run the double-precision kernel (no fused options)."""
     if inp.dtype == torch.float64:
         if (scale is not None or shift is not None or relu_mask or bn_stats is not None):
@@ -243,10 +272,9 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     lib = _lib.load()
     dev = inp.device
     gin = torch.empty_like(inp)
-    gx = torch.empty((C,), device=dev, dtype=_F32)
-    gy = torch.empty((C,), device=dev, dtype=_F32)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
+    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
     bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if bn_stats is not None else None
     nb = 4 * (gout.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
@@ -257,6 +285,8 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
                                  _ptr(bpart), _ptr(gin), _ptr(gx), _ptr(gy), _ptr(ws), nbytes,
                                  B, C, H, W, stride, int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd")
+    if pp is not None:
+        gx = pp
     if bn_stats is not None:
         return gin, gx, gy, bpart
     return gin, gx, gy
@@ -274,7 +304,7 @@ def ra_fits(n, V):
     return -(-n // ((nt // V) * V)) <= 32
 
 
-def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats"):
+def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats", defer_pos=False):
     """Shift_tcn.shift_in backward (stride 1, Shift_tcn.bn's affine on the taps and its
     backward partials) that also emits the k-free backward sums of Shift_gcn.bn, whose
     input is ``z`` and whose ReLU output is ``inp`` (sgcn_tshift_bwd_gbn). Returns
@@ -286,10 +316,9 @@ def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats"):
     lib = _lib.load()
     dev = inp.device
     gin = torch.empty_like(inp)
-    gx = torch.empty((C,), device=dev, dtype=_F32)
-    gy = torch.empty((C,), device=dev, dtype=_F32)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
+    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
     bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32)
     zpart = torch.empty((6 * B * C * W,), device=dev, dtype=_F32)
     nb = 4 * (gout.numel() + 3 * inp.numel())
@@ -300,13 +329,13 @@ def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats"):
                                      _ptr(zst.invstd), _ptr(zpart), _ptr(gin), _ptr(gx),
                                      _ptr(gy), _ptr(ws), nbytes, B, C, H, W, _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd_gbn")
-    return gin, gx, gy, bpart, zpart
+    return gin, (pp if pp is not None else gx), gy, bpart, zpart
 
 
 BNIN_MAX_PLANE = 16384   # sgcn_tshift_bwd_bnin: LDS-staged stride-1 planes only
 
 
-def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos):
+def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False):
     """Stride-1 shift backward (ReLU mask on ``inp``) whose output gradient is the input
     gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3, formed in the
     kernel (``s`` None: s = shift(inp), re-formed from its taps). Returns (grad_input,
@@ -315,17 +344,16 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos):
     lib = _lib.load()
     dev = inp.device
     gin = torch.empty_like(inp)
-    gx = torch.empty((C,), device=dev, dtype=_F32)
-    gy = torch.empty((C,), device=dev, dtype=_F32)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
+    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
     nb = 4 * ((2 + (s is not None)) * dy.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_bwd_bnin(_ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp),
                                       _ptr(xpos), _ptr(ypos), _ptr(gin), _ptr(gx), _ptr(gy),
                                       _ptr(ws), nbytes, B, C, H, W, 1, _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd_bnin")
-    return gin, gx, gy
+    return gin, (pp if pp is not None else gx), gy
 
 
 # --------------------------------------------------------------------------------------
