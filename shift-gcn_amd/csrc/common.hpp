@@ -89,6 +89,34 @@ __device__ __forceinline__ float shifted_at(const float* __restrict__ p, const S
   return q11 * omdx * omdy + q21 * g.dx * omdy + q12 * omdx * g.dy + q22 * g.dx * g.dy;
 }
 
+// Four floats at once (one barrier pair); `red` needs 4*blockDim.x/64 floats.
+__device__ __forceinline__ void block_sum4(float& a, float& b, float& c, float& d, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  d = wave_sum(d);
+  __syncthreads();
+  if (lane == 0) {
+    red[4 * wid] = a;
+    red[4 * wid + 1] = b;
+    red[4 * wid + 2] = c;
+    red[4 * wid + 3] = d;
+  }
+  __syncthreads();
+  float sa = 0.f, sb = 0.f, sc = 0.f, sd = 0.f;
+  for (int i = 0; i < nw; ++i) {
+    sa += red[4 * i];
+    sb += red[4 * i + 1];
+    sc += red[4 * i + 2];
+    sd += red[4 * i + 3];
+  }
+  a = sa;
+  b = sb;
+  c = sc;
+  d = sd;
+}
+
 // Chan et al. merge of (n, mean, M2) partial statistics, in double.
 struct Moments {
   double n, mean, m2;

@@ -566,7 +566,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   // sum over outputs, and the constraint keeps only the sign of the sum, .cu:370-395).
   constexpr bool RA = STRIDE == 1;
   extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input (STRIDE 2 only)]
-  __shared__ float red[2 * NT / 64];
+  __shared__ float red[4 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   const int nb = Hb * W, nt = Ho * W;
@@ -810,11 +810,15 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
       pos.next();
     }
   }
-  block_sum2(ax, ay, red);
-  if (threadIdx.x == 0) pgrad[plane] = make_float2(ax, ay);
-  if (BNP) {
-    block_sum2(bs0, bs1, red);
-    if (threadIdx.x == 0) bn_part[plane] = make_float2(bs0, bs1);
+  if (BNP) {   // both plane reductions behind one barrier pair
+    block_sum4(ax, ay, bs0, bs1, red);
+    if (threadIdx.x == 0) {
+      pgrad[plane] = make_float2(ax, ay);
+      bn_part[plane] = make_float2(bs0, bs1);
+    }
+  } else {
+    block_sum2(ax, ay, red);
+    if (threadIdx.x == 0) pgrad[plane] = make_float2(ax, ay);
   }
   if (GBN) {
     // merge the G = NTE / W row groups of each joint in fixed order (deterministic)
@@ -822,15 +826,14 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
 #pragma unroll
     for (int k = 0; k < 6; ++k) lds[k * NT + threadIdx.x] = a6[k];
     __syncthreads();
-    if ((int)threadIdx.x < W) {
+    // one thread per (sum k, joint w): G dependent LDS reads each instead of 6*G
+    if ((int)threadIdx.x < 6 * W) {
       const int G = NTE / W;
       const size_t np = (size_t)gridDim.x * W;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        float sum = 0.f;
-        for (int g = 0; g < G; ++g) sum += lds[k * NT + g * W + threadIdx.x];
-        gzpart[k * np + (size_t)plane * W + threadIdx.x] = sum;
-      }
+      const int k = (int)threadIdx.x / W, w = (int)threadIdx.x - k * W;
+      float sum = 0.f;
+      for (int g = 0; g < G; ++g) sum += lds[k * NT + g * W + w];
+      gzpart[k * np + (size_t)plane * W + w] = sum;
     }
   }
 }
@@ -985,6 +988,12 @@ int ra_lpt(int n, int nt, int W) {
   const int per = (n + nte - 1) / nte;
   return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
 }
+
+// largest stride-1 plane the joint-aligned backward kernels with affine taps (shift_in:
+// plain and GBN) run on 256-thread workgroups (up to 32 elements per thread): at NTU T=300
+// (7,500 floats) measured 8 % (GBN) / 4 % (plain) faster than 512 threads; the shift_out
+// backward (bnin) keeps 512 threads above 4,096 floats (no difference)
+constexpr int kRaSplit256 = 8192;
 
 int pick_ept(int n) {
   const int per = (n + kThreads - 1) / kThreads;
@@ -1191,7 +1200,7 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   // sgcn_tshift_bwd's stride-1 thread counts; elements per thread from the W-aligned
   // stride (NT / W) * W
   const int n = H * W;
-  const int ntg = n <= 4096 ? 256 : kBwdThreads;
+  const int ntg = n <= kRaSplit256 ? 256 : kBwdThreads;
   const int lpt = ra_lpt(n, ntg, W);
   SGCN_REQUIRE(lpt > 0);   // elements per thread within the largest LPT
   if (ntg == 256) {
@@ -1230,7 +1239,7 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
   // stride 1: joint-aligned LDS kernels (W <= 64, <= 32 elements per thread); small planes
   // (T = 150 / 75) on 256 threads, so fewer lanes idle per workgroup
-  const int nt1 = H * W <= 4096 ? 256 : kBwdThreads;
+  const int nt1 = H * W <= kRaSplit256 ? 256 : kBwdThreads;
   const int lpt1 = stride == 1 && H > 0 && H * W <= kBwdLdsMax ? ra_lpt(H * W, nt1, W) : 0;
   if (lpt1) {
 #define SGCN_BWD1(L, NTT)                                                                       \
