@@ -140,7 +140,7 @@ def gcn_forward(mod, x0, training, off=False):
     if mod.has_down:
         conv, bn = mod.down[0], mod.down[1]
         D0 = _empty(B, Cout, T, V, like=x0)
-        down = _OffPath(off, x0)
+        down = _OffPath(off and OFF_FWD, x0)
         with down:
             ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
             if training:
@@ -479,7 +479,7 @@ def unit_forward(unit, x, training):
     rs = None
     if unit.residual_kind == "conv":
         # the residual conv branch runs on the side stream, concurrently with Shift_tcn
-        res = _OffPath(off, x)
+        res = _OffPath(off and OFF_FWD, x)
         with res:
             Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
     so = unit.tcn1.shift_out
@@ -643,6 +643,8 @@ GCN_ZU = int(os.environ.get("SGCN_GCN_ZU", "1"))
 ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
 # ... with the small off-path kernels too (position-gradient finalize, next unit's mask)
 OFF_SMALL = int(os.environ.get("SGCN_OFF_SMALL", "1"))
+# ... and the forward's down / residual conv branches (A/B knob)
+OFF_FWD = int(os.environ.get("SGCN_OFF_FWD", "1"))
 # ... enqueued after the dX contraction of the same operand (A/B knob)
 DW_AFTER_DX = int(os.environ.get("SGCN_DW_AFTER_DX", "1"))
 # S-free unit tails in training (bn2's input re-formed from R; see unit_forward). A/B knob,
