@@ -542,8 +542,9 @@ def _off_path_ok(unit, s: UnitSaved):
     if not s.off or torch.cuda.is_current_stream_capturing():
         return False
     for p in unit.parameters():
-        if p.requires_grad and p.grad is not None:
-            return False
+        if p.requires_grad and (p.grad is not None or getattr(p, "_backward_hooks", None) or
+                                getattr(p, "_post_accumulate_grad_hooks", None)):
+            return False   # accumulation, or a hook that would read the gradient early
     # join at the end of this backward pass, before backward() returns (the engine runs
     # final callbacks on the caller's current stream)
     torch.autograd.Variable._execution_engine.queue_callback(

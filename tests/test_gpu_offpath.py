@@ -107,3 +107,26 @@ def test_existing_grad_accumulates_in_order():
             fused.ASYNC_DW = old
     for n in ref[0]:
         assert torch.equal(ref[0][n], ref[1][n]), n
+
+
+def test_parameter_hook_sees_finished_gradient():
+    """A gradient hook on a weight reads it during the backward: that unit must not use
+    the side stream (the hook would otherwise see an unwritten tensor)."""
+    from shiftgcn import fused
+    dev = torch.device("cuda:0")
+    x = formula.tensor((4, 3, 64, 25, 2), 43, 1.0).to(dev)
+    y = torch.tensor([1, 2, 3, 4], device=dev)
+    seen = {}
+    for mode in (0, 1):
+        old = fused.ASYNC_DW
+        fused.ASYNC_DW = mode
+        try:
+            m = _model(dev)
+            w = m.l9.tcn1.temporal_linear.weight
+            w.register_hook(lambda g, mode=mode: seen.__setitem__(mode, g.detach().clone()))
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            torch.cuda.synchronize()
+        finally:
+            fused.ASYNC_DW = old
+    assert torch.equal(seen[0], seen[1])
+
