@@ -15,6 +15,8 @@ hipGraph, so a batch costs one graph launch.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 from torch import nn
@@ -82,6 +84,18 @@ def derive_modalities(joint, parent, planes=False, data_bn=None, out=None):
     return out
 
 
+# one stream per ensemble member (A/B knob: SGCN_ENS_STREAMS=0 runs them in order)
+ENS_STREAMS = int(os.environ.get("SGCN_ENS_STREAMS", "1"))
+_ENS_STREAMS = {}
+
+
+def _ens_streams(device):
+    s = _ENS_STREAMS.get(device)
+    if s is None:
+        s = _ENS_STREAMS[device] = [torch.cuda.Stream(device=device) for _ in range(4)]
+    return s
+
+
 class Ensemble(nn.Module):
     """``run_ensemble_inference`` over a batch: ``forward(joint)`` -> ``(scores, logits)``
     with ``scores`` = softmax(fused logits)[:, 1] (P(fall) for the MediaPipe models) and
@@ -128,8 +142,24 @@ class Ensemble(nn.Module):
                                     data_bn=self._data_bn_coef())
         acc = torch.zeros(N, self.models[0].fc.out_features, device=joint.device,
                           dtype=torch.float64)
-        for k, (m, xs) in enumerate(zip(self.models, streams)):
-            logits = m.forward_planes(xs, N, M)
+        if ENS_STREAMS:
+            # the four models are independent until the fused score: each runs on its own
+            # stream (forked from and joined back into the current one; works inside a
+            # hipGraph capture), so their MFMA- and HBM-bound phases overlap; the logits
+            # are then accumulated in stream order as before
+            cur = torch.cuda.current_stream(joint.device)
+            subs = _ens_streams(joint.device)
+            outs = []
+            for m, xs, st in zip(self.models, streams, subs):
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    outs.append(m.forward_planes(xs, N, M))
+                xs.record_stream(st)
+            for st in subs:
+                cur.wait_stream(st)
+        else:
+            outs = [m.forward_planes(xs, N, M) for m, xs in zip(self.models, streams)]
+        for k, logits in enumerate(outs):
             acc = acc + (logits * self.alpha32[k]).double()
         # softmax exactly as inference_pipeline.py:364-365 (max-shifted exp in float64)
         e = torch.exp(acc - acc.max(dim=1, keepdim=True).values)
