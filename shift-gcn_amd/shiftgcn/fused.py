@@ -52,13 +52,12 @@ def _empty(*shape, like):
 # current stream before returning, so everything after loss.backward() sees finished grads.
 # --------------------------------------------------------------------------------------
 _SIDE = {}
-SIDE_PRIORITY = int(os.environ.get("SGCN_SIDE_PRIORITY", "0"))
 
 
 def _side_stream(device):
     s = _SIDE.get(device)
     if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device=device, priority=SIDE_PRIORITY)
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
     return s
 
 
