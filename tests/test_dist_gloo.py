@@ -58,8 +58,11 @@ def _worker(rank, world, port, q):
         m.bn.running_mean.fill_(float(rank + 7))
         GradAllReduce(m)()
         broadcast_buffers(m)
-        q.put((rank, m.lin.weight.grad.clone(), m.lin.bias.grad.clone(),
-               m.shift.ypos.grad.clone(), m.bn.running_mean.clone(), m.lin.weight.detach().clone()))
+        # numpy, not tensors: a tensor in a queue is shared through a socket owned by this
+        # process, which may already have exited when the parent unpickles it
+        q.put((rank,) + tuple(t.detach().numpy().copy() for t in (
+            m.lin.weight.grad, m.lin.bias.grad, m.shift.ypos.grad, m.bn.running_mean,
+            m.lin.weight)))
     finally:
         dist.destroy_process_group()
 
@@ -77,6 +80,7 @@ def test_grad_allreduce_dataparallel_rule_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort(key=lambda r: r[0])
+    res = [(r[0],) + tuple(torch.from_numpy(a) for a in r[1:]) for r in res]
     for rank, w, b, y, rm, wt in res:
         assert torch.allclose(w, torch.full_like(w, 1.5))            # mean of 1 and 2
         assert torch.allclose(b, torch.full_like(b, 15.0))           # mean of 10 and 20
