@@ -631,8 +631,10 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
 # the weight gradient re-forms it from H; 0: the round-1 two-launch form (shift launch +
 # contraction). A/B knob: SGCN_TSHIFT_FUSION=0|1|2.
 TSHIFT_FUSION = int(os.environ.get("SGCN_TSHIFT_FUSION", "1"))
-# fuse only from this many channels up (below, the two-launch form is used)
-TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "128"))
+# fuse only from this many channels up (below, the two-launch form is used). With the
+# weight gradients on the side stream, fusing the C = 128 units costs 0.3 % of the step and
+# the C = 256 units are neutral (same-box A/B, profiles/r02_close/ab_tshift_fusion.txt)
+TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "256"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
 # (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass. A/B knob.
 GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))

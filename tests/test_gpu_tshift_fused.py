@@ -94,16 +94,18 @@ def test_fused_weight_gradient_matches_materialised(case):
     assert float((db2 - db1).abs().max()) <= 1e-6 * float(db1.abs().max()) + 1e-7
 
 
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_unit_matches_oracle_in_every_fusion_mode(monkeypatch, mode):
-    """SGCN_TSHIFT_FUSION 0 (two launches) and 2 (weight gradient re-forms the operand)
-    give the same unit parity as the default mode 1 (tested by test_gpu_blocks)."""
+    """SGCN_TSHIFT_FUSION 0 (two launches), 1 (fused, shifted operand stored) and 2 (weight
+    gradient re-forms the operand) give the same unit parity, with the channel threshold
+    at 0 so the C = 128 unit below takes the fused form."""
     import formula
     import shiftgcn
     from oracle import model_oracle as mo
     from shiftgcn import fused
     from test_gpu_blocks import _compare
     monkeypatch.setattr(fused, "TSHIFT_FUSION", mode)
+    monkeypatch.setattr(fused, "TSHIFT_FUSION_MIN_C", 0)
     ref = mo.TCN_GCN_unit(64, 128, None, stride=2, num_point=25)
     formula.fill_state(ref, seed=mode + 17)
     ours = shiftgcn.TCN_GCN_unit(64, 128, None, stride=2, num_point=25).to(DEV)
