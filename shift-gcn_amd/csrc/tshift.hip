@@ -542,7 +542,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
 //   {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh} over t where H > 0,
 //   zh = (Z - zmean[c,v]) * zinvstd[c,v]; sgcn_bn_bwd_finalize_gbn combines them.
 template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP, bool GP = false,
-          bool GBN = false, bool SREC = false>
+          bool GBN = false, bool SREC = false, bool JA = false>
 __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
@@ -557,6 +557,13 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   static_assert(!GP || STRIDE == 1, "GP is a stride-1 (re-associated) variant");
   static_assert(!GBN || (STRIDE == 1 && BNP && !GP), "GBN: stride-1 shift_in with BNP");
   static_assert(!SREC || GP, "SREC: bn2's input re-formed in the GP staging");
+  // JA (stride 2): both planes staged as in the general path, but the two passes walk
+  // their grids on the joint-aligned element stride (NT / W) * W like the stride-1 kernels:
+  // a thread's joint w is fixed, so the column part of every tap is a per-thread constant,
+  // and of the two gout rows an input row can reach (h1 / 2 and (h1 + 1) / 2) exactly one
+  // exists, so pass (1) reads 2 taps, not 4 (the other two are the exact zeros the general
+  // path selects)
+  static_assert(!JA || STRIDE == 2, "JA: the stride-2 joint-aligned walk");
   // STRIDE == 1 ("re-associated"): only gout is staged (half the LDS -> twice the
   // workgroups per CU); each thread's own input elements are loaded into registers with
   // the staging loads, and the position-gradient sums are accumulated over INPUT positions
@@ -753,6 +760,34 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
         ay += qa * cy;
       }
     }
+  } else if (JA) {
+    const Geom r = make_geom(-x, -y);
+    const int NTJ = (NT / W) * W, GR = NT / W;
+    if ((int)threadIdx.x < NTJ && nt > 0) {
+      const int w = (int)threadIdx.x % W, w1 = w + r.x1;
+      const bool c0 = (unsigned)w1 < (unsigned)W, c1 = (unsigned)(w1 + 1) < (unsigned)W;
+      const int cc0 = min(max(w1, 0), W - 1), cc1 = min(max(w1 + 1, 0), W - 1);
+      int h = (int)threadIdx.x / W;
+      for (int o = threadIdx.x; o < nb; o += NTJ, h += GR) {
+        // input row h reaches gout row hq = h1 / 2 (h1 = h + y1 even: taps q11, q21) or
+        // (h1 + 1) / 2 (h1 odd: taps q12, q22); (h1 + 1) >> 1 is both, floor for h1 < 0
+        const int h1 = h + r.y1, hq = (h1 + 1) >> 1;
+        const bool ev = (h1 & 1) == 0, rok = (unsigned)hq < (unsigned)Ho;
+        const int ro = min(max(hq, 0), Ho - 1) * W;
+        const float t0 = (rok && c0) ? gs[ro + cc0] : 0.f;
+        const float t1 = (rok && c1) ? gs[ro + cc1] : 0.f;
+        float val = blend(ev ? t0 : 0.f, ev ? t1 : 0.f, ev ? 0.f : t0, ev ? 0.f : t1, r.dx, r.dy);
+        const float rin = xs[o];
+        if (RELU_MASK) val = rin > 0.f ? val : 0.f;
+        gi[o] = val;
+        if (BNP) {
+          bs0 += val;
+          bs1 += val * ((rin - bmu) * bis);
+        }
+      }
+    } else if ((int)threadIdx.x < NTJ) {   // no gout rows (Ho == 0): the gradient is 0
+      for (int o = threadIdx.x; o < nb; o += NTJ) gi[o] = 0.f;
+    }
   } else {
     const Geom r = make_geom(-x, -y);
     Walker pos(threadIdx.x, NT, W);
@@ -790,7 +825,32 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   }
 
   // (2) position gradients over the top grid (.cu:321-349), summed over the plane
-  if (!RA) {
+  if (JA) {
+    const Geom g = make_geom(x, y);
+    const int NTJ = (NT / W) * W, GR = NT / W;
+    if ((int)threadIdx.x < NTJ) {
+      const int w = (int)threadIdx.x % W, wc = w + g.x1;
+      const bool c0 = (unsigned)wc < (unsigned)W, c1 = (unsigned)(wc + 1) < (unsigned)W;
+      const int cc0 = min(max(wc, 0), W - 1), cc1 = min(max(wc + 1, 0), W - 1);
+      int h = (int)threadIdx.x / W;
+      for (int o = threadIdx.x; o < nt; o += NTJ, h += GR) {
+        const int rr = h * STRIDE + g.y1;
+        const bool r0 = (unsigned)rr < (unsigned)Hb, r1 = (unsigned)(rr + 1) < (unsigned)Hb;
+        const int p0 = min(max(rr, 0), Hb - 1) * W, p1 = min(max(rr + 1, 0), Hb - 1) * W;
+        float q11 = xs[p0 + cc0], q21 = xs[p0 + cc1], q12 = xs[p1 + cc0], q22 = xs[p1 + cc1];
+        if (AFFINE) { q11 = q11 * a + b; q21 = q21 * a + b; q12 = q12 * a + b; q22 = q22 * a + b; }
+        q11 = (r0 && c0) ? q11 : 0.f;
+        q21 = (r0 && c1) ? q21 : 0.f;
+        q12 = (r1 && c0) ? q12 : 0.f;
+        q22 = (r1 && c1) ? q22 : 0.f;
+        const float vx = (1.f - g.dy) * (q21 - q11) + g.dy * (q22 - q12);
+        const float vy = (1.f - g.dx) * (q12 - q11) + g.dx * (q22 - q21);
+        const float gg = gs[o];
+        ax += vx * gg;
+        ay += vy * gg;
+      }
+    }
+  } else if (!RA) {
     const Geom g = make_geom(x, y);
     Walker pos(threadIdx.x, NT, W);
     for (int o = threadIdx.x; o < nt; o += NT) {
@@ -948,7 +1008,7 @@ void launch_bwd(bool affine, bool relu, const float* gout, const float* in, cons
 
 constexpr int kBwdThreads = 512;
 
-template <int LPT, int STRIDE, int NT = kBwdThreads>
+template <int LPT, int STRIDE, int NT = kBwdThreads, bool JA = false>
 void launch_bwd_lds(bool affine, bool relu, const float* gout, const float* in,
                     const float* xpos, const float* ypos, const float* scale,
                     const float* shift, const float* bmu, const float* bis, float* gin,
@@ -957,8 +1017,9 @@ void launch_bwd_lds(bool affine, bool relu, const float* gout, const float* in,
   dim3 grid(B * C), block(NT);
   const size_t lds = (size_t)(STRIDE == 1 ? Ho : H + Ho) * W * sizeof(float);
 #define SGCN_BWDL(A, R, P)                                                                  \
-  tshift_bwd_lds_kernel<NT, LPT, A, R, STRIDE, P><<<grid, block, lds, st>>>(               \
-      gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, Ho, add_half)
+  tshift_bwd_lds_kernel<NT, LPT, A, R, STRIDE, P, false, false, false, JA>                  \
+      <<<grid, block, lds, st>>>(gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, \
+                                 H, W, Ho, add_half)
   if (bp) {
     if (affine) {
       if (relu) SGCN_BWDL(true, true, true); else SGCN_BWDL(true, false, true);
@@ -1259,10 +1320,16 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   }
   if (stride == 2 && (H + Ho) * W <= kBwdLdsMax && H > 0) {
     const int lpt = pick_lpt((H + Ho) * W, kBwdThreads);
-#define SGCN_BWDL_LPT(L)                                                                      \
-  launch_bwd_lds<L, 2>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, \
-                       gin, pg, bp, B, C, H, W, Ho, ah, st)
-    if (lpt == 8) SGCN_BWDL_LPT(8); else if (lpt == 16) SGCN_BWDL_LPT(16); else SGCN_BWDL_LPT(32);
+#define SGCN_BWDL_LPT(L, J)                                                                   \
+  launch_bwd_lds<L, 2, kBwdThreads, J>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,     \
+                                       bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st)
+    if (W <= 64) {   // joint-aligned walk (W <= NT)
+      if (lpt == 8) SGCN_BWDL_LPT(8, true); else if (lpt == 16) SGCN_BWDL_LPT(16, true);
+      else SGCN_BWDL_LPT(32, true);
+    } else {
+      if (lpt == 8) SGCN_BWDL_LPT(8, false); else if (lpt == 16) SGCN_BWDL_LPT(16, false);
+      else SGCN_BWDL_LPT(32, false);
+    }
 #undef SGCN_BWDL_LPT
   } else {
   const int ept = pick_ept(H * W);

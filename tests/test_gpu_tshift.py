@@ -47,7 +47,9 @@ def test_shift_matches_golden_bit_exact(golden, case):
                                    (2, 8, 300, 33), (1, 4, 600, 25),
                                    # planes too large for the LDS-staged kernels: the
                                    # global-tap kernels must agree bit for bit too
-                                   (1, 4, 700, 25)])
+                                   (1, 4, 700, 25),
+                                   # W > 64: the general (non joint-aligned) LDS walk
+                                   (1, 4, 40, 70)])
 def test_shift_matches_oracle_bit_exact(shape, stride):
     B, C, H, W = shape
     rng = np.random.default_rng(B * 1000 + C * 10 + H + stride)

@@ -9,7 +9,7 @@ O=gpurun_out/abenv
 mkdir -p $O
 for r in $(seq 1 ${REPS:-2}); do
   for c in $CASES; do
-    tag=$(echo $c | tr ',=' '__')
+    tag=$(echo $c | tr ',=/.' '____')
     env $(echo $c | tr ',' ' ') timeout -k 10 300 python -u bench.py --cpu-baseline 0 ${BENCH_ARGS} > $O/${tag}_$r.log 2>&1 || { tail -20 $O/${tag}_$r.log; exit 1; }
     echo "$c run $r: $(python3 -c "import json; d=json.loads(open('$O/${tag}_$r.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])")"
   done
