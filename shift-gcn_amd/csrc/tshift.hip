@@ -339,7 +339,10 @@ __device__ __forceinline__ void stage_plane(const float* __restrict__ src, float
   }
 }
 
-template <int NT, int EPT, int LPT, bool AFFINE, bool STATS>
+// JA: output elements dealt on the joint-aligned stride (NT / W) * W (as the stride-1
+// backward kernels), so the column part of the four taps is a per-thread constant and only
+// the rows are range-checked per element; the values are the same expression
+template <int NT, int EPT, int LPT, bool AFFINE, bool STATS, bool JA = false>
 __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
     const float* __restrict__ ypos, const float* __restrict__ scale,
@@ -361,23 +364,45 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
   __syncthreads();
   const int n = Ho * W;
   double run_n = 0.0, run_mean = 0.0, run_m2 = 0.0;  // block-uniform (STATS only)
-  for (int base = 0; base < n; base += EPT * NT) {
+  const int NTJ = JA ? (NT / W) * W : NT, GR = NT / W;
+  const bool own = !JA || (int)threadIdx.x < NTJ;
+  const int wj = (int)threadIdx.x % W, wc = wj + g.x1;
+  const bool c0 = (unsigned)wc < (unsigned)W, c1 = (unsigned)(wc + 1) < (unsigned)W;
+  const int cc0 = min(max(wc, 0), W - 1), cc1 = min(max(wc + 1, 0), W - 1);
+  for (int base = 0; base < n; base += EPT * NTJ) {
     float v[EPT];
-    Walker pos(base + threadIdx.x, NT, W);
+    if (JA) {
+      int h = base / W + (int)threadIdx.x / W;
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      TapIdx ti;
-      tap_idx(pos.h * stride + g.y1, pos.w + g.x1, Hb, W, ti);
-      const float q11 = sel(pl[ti.o00], ti.m00), q21 = sel(pl[ti.o01], ti.m01);
-      const float q12 = sel(pl[ti.o10], ti.m10), q22 = sel(pl[ti.o11], ti.m11);
-      const int o = base + e * NT + threadIdx.x;
-      const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
-      v[e] = o < n ? val : 0.f;
-      if (store && o < n) dst[o] = val;
-      pos.next();
+      for (int e = 0; e < EPT; ++e, h += GR) {
+        const int o = base + e * NTJ + threadIdx.x;
+        const int rr = h * stride + g.y1;
+        const bool r0 = (unsigned)rr < (unsigned)Hb, r1 = (unsigned)(rr + 1) < (unsigned)Hb;
+        const int p0 = min(max(rr, 0), Hb - 1) * W, p1 = min(max(rr + 1, 0), Hb - 1) * W;
+        const float q11 = (r0 && c0) ? pl[p0 + cc0] : 0.f, q21 = (r0 && c1) ? pl[p0 + cc1] : 0.f;
+        const float q12 = (r1 && c0) ? pl[p1 + cc0] : 0.f, q22 = (r1 && c1) ? pl[p1 + cc1] : 0.f;
+        const bool ok = own && o < n;
+        const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
+        v[e] = ok ? val : 0.f;
+        if (store && ok) dst[o] = val;
+      }
+    } else {
+      Walker pos(base + threadIdx.x, NT, W);
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        TapIdx ti;
+        tap_idx(pos.h * stride + g.y1, pos.w + g.x1, Hb, W, ti);
+        const float q11 = sel(pl[ti.o00], ti.m00), q21 = sel(pl[ti.o01], ti.m01);
+        const float q12 = sel(pl[ti.o10], ti.m10), q22 = sel(pl[ti.o11], ti.m11);
+        const int o = base + e * NT + threadIdx.x;
+        const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
+        v[e] = o < n ? val : 0.f;
+        if (store && o < n) dst[o] = val;
+        pos.next();
+      }
     }
     if (STATS) {
-      const int cnt = min(n - base, EPT * NT);
+      const int cnt = min(n - base, EPT * NTJ);
       float s = 0.f;
 #pragma unroll
       for (int e = 0; e < EPT; ++e) s += v[e];
@@ -386,9 +411,9 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
       float m2 = 0.f;
 #pragma unroll
       for (int e = 0; e < EPT; ++e) {
-        const int o = base + e * NT + threadIdx.x;
+        const int o = base + e * NTJ + threadIdx.x;
         const float d = v[e] - mean;
-        m2 += (o < n) ? d * d : 0.f;
+        m2 += (own && o < n) ? d * d : 0.f;
       }
       m2 = block_sum(m2, red);
       const Moments m = merge({run_n, run_mean, run_m2}, {(double)cnt, (double)mean, (double)m2});
@@ -970,13 +995,21 @@ void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const 
                     hipStream_t st) {
   dim3 grid(B * C), block(NT);
   const size_t lds = (size_t)H * W * sizeof(float);
-#define SGCN_FWDL(A, S)                                                                  \
-  tshift_fwd_lds_kernel<NT, LPT, LPT, A, S><<<grid, block, lds, st>>>(                  \
+#define SGCN_FWDL(A, S, J)                                                               \
+  tshift_fwd_lds_kernel<NT, LPT, LPT, A, S, J><<<grid, block, lds, st>>>(               \
       in, out, xpos, ypos, scale, shift, ps, C, H, W, Ho, stride, add_half)
-  if (affine) {
-    if (stats) SGCN_FWDL(true, true); else SGCN_FWDL(true, false);
+  if (W <= 64) {   // joint-aligned element stride (W <= NT)
+    if (affine) {
+      if (stats) SGCN_FWDL(true, true, true); else SGCN_FWDL(true, false, true);
+    } else {
+      if (stats) SGCN_FWDL(false, true, true); else SGCN_FWDL(false, false, true);
+    }
   } else {
-    if (stats) SGCN_FWDL(false, true); else SGCN_FWDL(false, false);
+    if (affine) {
+      if (stats) SGCN_FWDL(true, true, false); else SGCN_FWDL(true, false, false);
+    } else {
+      if (stats) SGCN_FWDL(false, true, false); else SGCN_FWDL(false, false, false);
+    }
   }
 #undef SGCN_FWDL
 }
