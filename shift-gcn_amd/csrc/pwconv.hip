@@ -191,8 +191,10 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   constexpr int KSTEP_B = NT / BN;
   static_assert(MI >= 1 && NJ >= 1 && A_PER >= 1 && B_PER >= 1, "bad tile");
   static_assert((BM * BK) % NT == 0 && NT % BN == 0 && NT % BK == 0 && NT % BM == 0, "bad tile");
-  __shared__ float As[2][BK * AP];
-  __shared__ float Bs[2][BK * BP];
+  // operand stages; the epilogue reuses the same memory to stage the accumulator tile
+  __shared__ float smem[2 * BK * AP + 2 * BK * BP];
+  float (*As)[BK * AP] = reinterpret_cast<float (*)[BK * AP]>(smem);
+  float (*Bs)[BK * BP] = reinterpret_cast<float (*)[BK * BP]>(smem + 2 * BK * AP);
   __shared__ float bias_s[BM];
   __shared__ int rot_s[BM];
   __shared__ unsigned ycol_s[BN];   // per tile column: byte offset of (b, t) in Y
@@ -377,52 +379,64 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   }
 
   SGCN_PW_STAMP(2);
-  // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5) ----
+  // ---- epilogue. The MFMA C/D map (col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5))
+  // leaves each wave holding 32-column pieces of 64 rows; stored straight from registers,
+  // a 128-B line of a Y row is completed by several waves (and tiles) at different times,
+  // and lines evicted from L2 half-written cost a second partial write (PMC: 1.20x the
+  // algorithmic bytes at M >= 128). So the tile is staged through LDS in passes of 16
+  // rows per wave band, and each wave then stores whole tile rows: 64 lanes on 64
+  // consecutive positions, BN/64 instructions per row, every line completed at once.
   const auto yr = make_rsrc(p.y.ptr, p.y_bytes);
   const unsigned ycs4 = (unsigned)(p.y.cstride * 4);
-  const bool slow = p.y.rsign != 0 || m0 + BM > M;
-  const int rbase = wm * (BM / WM) + 4 * kl;   // row of register 0 of sub-tile 0 (tile-local)
+  constexpr int NW = WM * WN;
+  constexpr int RB = WM * 16;      // staged rows per pass
+  constexpr int CQ = BN / 64;      // 64-column groups per row
+  static_assert(BN % 64 == 0 && RB * BN <= 2 * BK * (AP + BP), "epilogue staging");
+  unsigned ycolq[CQ];
+  int vq[CQ];
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) {
+    ycolq[q] = ycol_s[lane + 64 * q];
+    vq[q] = v_s[lane + 64 * q];
+  }
+  const bool rotated = p.y.rsign != 0;
   auto epilogue = [&](auto relu_tag) {
     constexpr bool RELU = decltype(relu_tag)::value;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int cidx = wn * (BN / WN) + j * 32 + cl;
-      const unsigned ycol = ycol_s[cidx];
-      const int v = v_s[cidx];
-      const unsigned lanerow = (unsigned)(4 * kl) * ycs4;
-      if (!slow) {
-        const unsigned voff = ycol + (unsigned)(v * 4) + lanerow;
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+      for (int h = 0; h < 2; ++h) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2);   // uniform
-            const unsigned soff = (unsigned)(m0 + rl) * ycs4;
-            float val = acc[i][j][r] + bias_s[rbase + i * 32 + (r & 3) + 8 * (r >> 2)];
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 8; ++rr) {
+            const int r = 8 * h + rr;
+            const int lr = wm * 16 + (r & 3) + 8 * ((r >> 2) & 1) + 4 * kl;
+            smem[lr * BN + wn * (BN / WN) + j * 32 + cl] = acc[i][j][r];
+          }
+        __syncthreads();
+        for (int lr = wid; lr < RB; lr += NW) {
+          const int trow = (lr >> 4) * (BM / WM) + i * 32 + 16 * h + (lr & 15);   // uniform
+          if (m0 + trow >= M) break;   // rows past M (lr increases with trow)
+          const float bv = bias_s[trow];
+          const int rot = rot_s[trow];
+          const unsigned soff = (unsigned)(m0 + trow) * ycs4;
+#pragma unroll
+          for (int q = 0; q < CQ; ++q) {
+            int vo = vq[q];
+            if (rotated) {   // shift_out rotation of the stored joint
+              vo += rot;
+              vo = vo >= V ? vo - V : vo;
+            }
+            const unsigned voff = ycolq[q] + (unsigned)(vo * 4);
+            float val = smem[lr * BN + lane + 64 * q] + bv;
             if (RELU) val = fmaxf(val, 0.f);
             if (ACCUM) val += bload(yr, voff, soff);
             bstore(yr, val, voff, soff);
           }
-      } else {
-        // shift_out rotation of the stored joint and/or rows past M
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2);   // uniform
-            const int row = rl + 4 * kl;
-            int vo = v + rot_s[row];
-            vo = vo >= V ? vo - V : vo;
-            const unsigned voff =
-                (m0 + row < M ? ycol + (unsigned)(vo * 4) : p.y_bytes) + lanerow;
-            const unsigned soff = (unsigned)(m0 + rl) * ycs4;
-            float val = acc[i][j][r] + bias_s[row];
-            if (RELU) val = fmaxf(val, 0.f);
-            if (ACCUM) val += bload(yr, voff, soff);
-            bstore(yr, val, voff, soff);
-          }
+        }
+        __syncthreads();
       }
-    }
   };
   if (p.relu) epilogue(std::true_type{});
   else epilogue(std::false_type{});

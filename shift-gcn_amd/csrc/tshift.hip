@@ -1294,9 +1294,13 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   // sgcn_tshift_bwd's stride-1 thread counts; elements per thread from the W-aligned
   // stride (NT / W) * W
   const int n = H * W;
-  const int ntg = n <= kRaSplit256 ? 256 : kBwdThreads;
-  const int lpt = ra_lpt(n, ntg, W);
-  SGCN_REQUIRE(lpt > 0);   // elements per thread within the largest LPT
+  int ntg = n <= kRaSplit256 ? 256 : kBwdThreads;
+  int lpt = ra_lpt(n, ntg, W);
+  if (lpt == 0 && ntg == 256) {   // > 32 elements per thread on 256: take 512 threads
+    ntg = kBwdThreads;
+    lpt = ra_lpt(n, ntg, W);
+  }
+  SGCN_REQUIRE(lpt > 0);   // elements per thread within the largest LPT (ops.ra_fits)
   if (ntg == 256) {
     if (lpt == 8) SGCN_GBN(256, 8);
     else if (lpt == 16) SGCN_GBN(256, 16);

@@ -127,6 +127,12 @@ class DeviceBatchLoader:
         # data-parallel shard: every rank draws the same global order (same seed) of
         # batch_size*world_size batches and takes its slice of each
         self.rank, self.world_size = int(rank), int(world_size)
+        if self.world_size > 1 and not drop_last:
+            # a short last global batch would give the ranks unequal (or empty) shards: a
+            # rank with an extra step then waits forever in the gradient all-reduce, and the
+            # 1/world mean of GradAllReduce assumes equal shards
+            raise ValueError("DeviceBatchLoader: world_size > 1 needs drop_last=True "
+                             "(every rank must run the same number of equal batches)")
         self.shuffle, self.drop_last = shuffle, drop_last
         self.device = torch.device(device)
         self.depth = max(1, int(depth))
@@ -141,8 +147,7 @@ class DeviceBatchLoader:
         batches = loader_order(len(self.feeder), bs * self.world_size, self.shuffle,
                                self.drop_last, self.generator)
         if self.world_size > 1:
-            batches = [b[r * bs:(r + 1) * bs] for b in batches]
-            batches = [b for b in batches if b]
+            batches = [b[r * bs:(r + 1) * bs] for b in batches]   # full global batches
         if not batches:
             return
         data = self.feeder.data

@@ -540,6 +540,10 @@ def _off_path_ok(unit, s: UnitSaved):
     without launching anything on the current stream before the join)."""
     if not s.off or torch.cuda.is_current_stream_capturing():
         return False
+    if torch.is_grad_enabled():
+        # backward(create_graph=True): AccumulateGrad clones the gradient on the current
+        # stream instead of taking it, before the side stream would have written it
+        return False
     for p in unit.parameters():
         if p.requires_grad and (p.grad is not None or getattr(p, "_backward_hooks", None) or
                                 getattr(p, "_post_accumulate_grad_hooks", None)):

@@ -297,7 +297,10 @@ GBN_MAX_PLANE = 16384    # sgcn_tshift_bwd_gbn: LDS-staged stride-1 planes only
 
 def ra_fits(n, V):
     """Whether a stride-1 plane of n = T*V elements fits the joint-aligned LDS backward
-    kernels (sgcn_tshift_bwd_bnin / _gbn): V <= 64, <= 32 elements per thread."""
+    kernels (sgcn_tshift_bwd_bnin / _gbn): V <= 64, <= 32 elements per thread. bnin runs
+    256 threads up to 4,096 floats and 512 above; gbn runs 256 up to 8,192 floats but
+    takes 512 whenever 256 would need more than 32 elements per thread, so both launch
+    every plane this accepts."""
     if V > 64 or n > GBN_MAX_PLANE:
         return False
     nt = 256 if n <= 4096 else 512

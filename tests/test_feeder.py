@@ -123,3 +123,13 @@ def test_device_loader_shards_global_batches(tmp_path):
                                            rank=r, world_size=2)])
     assert len(DeviceBatchLoader(f, 3, drop_last=True, device="cpu", world_size=2)) == 2
     assert [a + b for a, b in zip(*per_rank)] == glob
+
+
+def test_device_loader_refuses_uneven_shards(tmp_path):
+    """world_size > 1 without drop_last would hand the ranks unequal shards of the last
+    global batch (a rank with an extra step hangs in the all-reduce): refused up front."""
+    dp, lp, *_ = _write(tmp_path, n=17)
+    f = Feeder(dp, lp)
+    with pytest.raises(ValueError, match="drop_last"):
+        DeviceBatchLoader(f, 3, drop_last=False, device="cpu", rank=0, world_size=2)
+    assert len(DeviceBatchLoader(f, 3, drop_last=False, device="cpu")) == 6   # 1 rank: fine

@@ -130,3 +130,30 @@ def test_parameter_hook_sees_finished_gradient():
             fused.ASYNC_DW = old
     assert torch.equal(seen[0], seen[1])
 
+
+
+def test_create_graph_backward_stays_in_order():
+    """backward(create_graph=True) runs the units' backward with grad mode on, where
+    AccumulateGrad clones a gradient on the current stream instead of taking it: the side
+    stream must not be used, and the gradients equal a plain backward's."""
+    from shiftgcn import fused
+    dev = torch.device("cuda:0")
+    x = formula.tensor((4, 3, 64, 25, 2), 44, 1.0).to(dev)
+    y = torch.tensor([3, 1, 4, 1], device=dev)
+    res = {}
+    for mode, cg in ((0, False), (1, True)):
+        old = fused.ASYNC_DW
+        fused.ASYNC_DW = mode
+        try:
+            m = _model(dev)
+            for p in m.parameters():
+                p.grad = None
+            torch.nn.functional.cross_entropy(m(x), y).backward(create_graph=cg)
+            torch.cuda.synchronize()
+            res[mode] = {n: p.grad.detach().cpu() for n, p in m.named_parameters()
+                         if p.grad is not None}
+        finally:
+            fused.ASYNC_DW = old
+    assert res[0].keys() == res[1].keys() and len(res[0]) > 100
+    for n in res[0]:
+        assert torch.equal(res[0][n], res[1][n]), n
