@@ -22,9 +22,11 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 18
+#define SGCN_ABI_VERSION 19
 
-/* ABI version of the loaded library (== SGCN_ABI_VERSION). */
+/* ABI version of the loaded library (== SGCN_ABI_VERSION). 19: the measured-and-rejected
+ * variants are gone (the S-free unit tail's statistics-only shift and re-formed bn2 input,
+ * the re-forming temporal-shift weight gradient, per_joint = 1 / 2 rotated-store layouts). */
 int sgcn_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
@@ -43,8 +45,6 @@ int sgcn_abi_version(void);
  *   (a fused BatchNorm apply); both NULL = identity.
  * plane_stats: optional (B*C) float2 {mean, M2} of each output plane (n = H/stride*W),
  *   consumed by sgcn_bn_finalize(); NULL = not computed.
- * out == NULL (with plane_stats, planes with H*W <= 16384): statistics only, the shift
- *   output is not written (the training unit tail re-forms it: sgcn_tshift_fwd_tail).
  * Unlike the reference (at::zeros + kernel), every output element is written exactly
  * once (no memset pass). */
 int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float* ypos,
@@ -67,12 +67,9 @@ int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const flo
  * + res), res = 0 (r NULL), r (identity residual) or r*r_scale[c] + r_shift[c] (residual
  * tcn conv output with its eval BN), r laid out like out. gather_m/out_gathered (both or
  * neither): also out_gathered = sgcn_gcn_gather(out, gather_m) for the next unit. The
- * shifted tensor itself is never written. post_scale/post_shift are bn2's apply
- * coefficients: eval-mode (sgcn_bn_eval_coef) for inference, or training-mode batch
- * statistics from sgcn_tshift_fwd(out = NULL, plane_stats) + sgcn_bn_finalize (the
- * backward then re-forms bn2's input: sgcn_tshift_bwd_bnin with s = NULL,
- * sgcn_gcn_dx_finish / sgcn_bn_bwd_reduce with the shift positions). Planes with
- * H*W <= 16384 only (else SGCN_EINVAL: use sgcn_tshift_fwd + sgcn_bn_apply). */
+ * shifted tensor itself is never written. post_scale/post_shift are bn2's eval-mode
+ * apply coefficients (sgcn_bn_eval_coef): the inference tail. Planes with H*W <= 16384
+ * only (else SGCN_EINVAL: use sgcn_tshift_fwd + sgcn_bn_apply). */
 int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const float* ypos,
                          const float* post_scale, const float* post_shift, const float* r,
                          const float* r_scale, const float* r_shift, const float* gather_m,
@@ -83,10 +80,10 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
  * gradient of the BatchNorm that follows the shift inside a TCN_GCN_unit (Shift_tcn.bn2,
  * shift_gcn.py:73,161-162), formed while staging: gout = k1*(y > 0 ? dy : 0) + k2*s + k3
  * with dy/y the unit's output gradient/output, s = bn2's input, coef = [3][C] {k1,k2,k3}
- * from sgcn_bn_bwd_finalize. That gradient tensor is never written. s == NULL: bn2's
- * input is shift(in) itself (never stored), re-formed from in's taps. Same plane limits as
- * sgcn_tshift_bwd_gbn: H*W <= 16384, W <= 64, <= 32 elements per thread (else
- * SGCN_EINVAL: use sgcn_bn_bwd_apply + sgcn_tshift_bwd). */
+ * from sgcn_bn_bwd_finalize. That gradient tensor is never written. Plane limits:
+ * H*W <= 16384, W <= 64, <= 32 elements per thread of the joint-aligned stride (NT / W) * W,
+ * NT = 256 (H*W <= 4096) or 512 (else SGCN_EINVAL: use sgcn_bn_bwd_apply +
+ * sgcn_tshift_bwd). */
 int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const float* coef,
                          const float* in, const float* xpos, const float* ypos, float* gin,
                          float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
@@ -149,8 +146,8 @@ int sgcn_tshift_bwd_f64(const double* gout, const double* in, const double* xpos
  * statistics in the per-joint local order. Feed z_part to
  * sgcn_bn_bwd_finalize_gbn; no separate sgcn_bn_bwd_reduce pass over (gin, in, z).
  * H*W <= 16384, W <= 64 and at most 32 elements per thread of the joint-aligned stride
- * (NT / W) * W, NT = 256 (H*W <= 4096) or 512 (else SGCN_EINVAL: use sgcn_tshift_bwd +
- * sgcn_bn_bwd_reduce). */
+ * (NT / W) * W, NT = 256 (H*W <= 8192; 512 if 256 would need more than 32) or 512 (else
+ * SGCN_EINVAL: use sgcn_tshift_bwd + sgcn_bn_bwd_reduce). */
 int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
                         const float* ypos, const float* in_scale, const float* in_shift,
                         const float* bn_mean, const float* bn_invstd, float* bn_part,
@@ -188,8 +185,8 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
  * The shifted operand is formed from four taps of X while the contraction stages its
  * tiles (same arithmetic as sgcn_tshift_fwd, so Y is bit-identical to sgcn_tshift_fwd +
  * sgcn_pw_fwd); it is never read back from memory. x_shifted (optional, layout of x):
- * also store S there from the same registers (the weight gradient's operand; NULL = not
- * written, and sgcn_pw_dw_tshift re-forms it instead). w is (M, K) k-contiguous (Conv2d
+ * also store S there from the same registers (the weight gradient's operand, for
+ * sgcn_pw_dw; NULL = not written). w is (M, K) k-contiguous (Conv2d
  * weight); relu != 0 applies ReLU. Workspace: sgcn_pw_tshift_ws_bytes(K) (the per-channel
  * shift table). */
 size_t sgcn_pw_tshift_ws_bytes(int K);
@@ -203,18 +200,6 @@ int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long l
 /* Workspace bytes for sgcn_pw_dw. */
 size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V);
 
-/* Weight gradient of the fused Shift_tcn contraction (sgcn_pw_fwd_tshift): as sgcn_pw_dw
- * with X'(b,c,n) = shift_c(in_scale[c] * X[b][c] + in_shift[c])(n) formed from four taps
- * of X while staging (the shifted tensor is never read or written); G plain. Workspace:
- * sgcn_pw_dw_tshift_ws_bytes (shift table + deterministic split-K slabs). */
-size_t sgcn_pw_dw_tshift_ws_bytes(int B, int M, int Nc, int T, int V);
-int sgcn_pw_dw_tshift(const float* g, long long g_bstride, long long g_cstride, const float* x,
-                      long long x_bstride, long long x_cstride, const float* xpos,
-                      const float* ypos, const float* in_scale, const float* in_shift,
-                      float* dw, int dw_transpose, int dw_accumulate, float* dbias,
-                      int dbias_accumulate, void* ws, size_t ws_bytes, int B, int M, int Nc,
-                      int T, int V, void* stream);
-
 /* Weight gradient over every position: dW[m][c] (+)= sum_{b,n} G(b,m,n) * X'(b,c,n)
  * (stored [c][m] when dw_transpose, e.g. Linear_weight's (C_in, C_out) layout) and
  * dbias[m] (+)= sum_{b,n} G(b,m,n) (dbias may be NULL). Deterministic split-K. */
@@ -227,16 +212,16 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
 /* ------------------------------------------------------------------------------------
  * Training-mode BatchNorm (shift_gcn.py:38,55-56,85,99,137) and unit tails
  * ------------------------------------------------------------------------------------
- * per_joint = 1: BatchNorm1d(V*C) over (n, t) of a (B, C, T, V) tensor, feature
- * f = c*V + v here, reference feature index v*C + c (pass perm_V = V to finalize);
- * per_joint = 3: the same BatchNorm1d on the Shift_gcn contraction output stored BEFORE
- * its shift_out (sgcn_pw_fwd with y_rsign = 0): element (c, t, v) of that tensor is the
- * logical element (c, t, (v + c) mod V) (shift_gcn.py:114-118,136), so the rotation is
- * applied by these kernels' addressing instead of by the contraction's stores
- * (sgcn_moments, sgcn_bn_apply: outputs/residual/coefficients at the logical position;
- * sgcn_bn_bwd_reduce, sgcn_bn_bwd_apply: x read at the pre-rotation position; the latter
- * also stores dx there, as per_joint = 2);
- * per_joint = 0: BatchNorm2d, feature = channel. */
+ * per_joint = 3: Shift_gcn.bn, BatchNorm1d(V*C) over (n, t) (feature f = c*V + v here,
+ * reference feature index v*C + c: pass perm_V = V to the finalizes), on the Shift_gcn
+ * contraction output Z stored BEFORE its shift_out (sgcn_pw_fwd with y_rsign = 0):
+ * element (c, t, v) of Z is the logical element (c, t, (v + c) mod V)
+ * (shift_gcn.py:114-118,136), so the rotation is applied by these kernels' addressing
+ * instead of by the contraction's stores (sgcn_moments, sgcn_bn_apply: statistics /
+ * outputs / residual / coefficients at the logical position; sgcn_bn_bwd_reduce,
+ * sgcn_bn_bwd_apply: Z read at the pre-rotation position, and the latter stores dZ there,
+ * so the dW / dX contractions read it as a plain plane);
+ * per_joint = 0: BatchNorm2d, feature = channel. Other values: SGCN_EINVAL. */
 
 /* Bytes of the per-(b, feature) partials written by sgcn_moments / sgcn_bn_bwd_reduce. */
 size_t sgcn_moments_ws_bytes(int B, int C, int V, int per_joint);
@@ -275,16 +260,11 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
  * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none).
  * dy_coef (optional, [3][C], requires relu): dy is replaced by k1[c]*dy + k2[c]*y + k3[c],
  * i.e. the input gradient of the following BatchNorm2d (whose input is y), computed on the
- * fly instead of materialised (Shift_tcn.bn's dx feeding Shift_gcn's ReLU/BN backward).
- * x_xpos/x_ypos (optional, both or neither; per_joint = 0, relu, no r / dy_coef): the
- * BatchNorm input is the stride-1 temporal shift of `x` with these positions, never
- * written (a TCN_GCN_unit's bn2 input, see sgcn_tshift_fwd_tail); each element is
- * re-formed from four taps of x, bit-identical to sgcn_tshift_fwd's output. */
+ * fly instead of materialised (Shift_tcn.bn's dx feeding Shift_gcn's ReLU/BN backward). */
 int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x,
-                       const float* x_xpos, const float* x_ypos, const float* mean,
-                       const float* invstd, int per_joint, const float* r, const float* rmean,
-                       const float* rinvstd, const float* dy_coef, float* part, float* rpart,
-                       int B, int C, int T, int V, void* stream);
+                       const float* mean, const float* invstd, int per_joint, const float* r,
+                       const float* rmean, const float* rinvstd, const float* dy_coef,
+                       float* part, float* rpart, int B, int C, int T, int V, void* stream);
 
 /* dgamma/dbeta (+)= sums (reference feature order); coef[3][F] = {k1, k2, k3} such that
  * dx = k1*g + k2*x + k3: the training-mode BatchNorm input gradient (batch_stats = 1), or
@@ -306,9 +286,7 @@ int sgcn_bn_bwd_finalize_gbn(const float* part6, int B, int C, int V, long long 
                              void* stream);
 
 /* dx = k1*g + k2*x + k3; dr = g (rcoef NULL, dr given) or rk1*g + rk2*r + rk3;
- * dy_coef as in sgcn_bn_bwd_reduce. per_joint = 2: per-joint coefficients AND dx written
- * in the gathered layout dx[b,c,t,(v - c) mod V] (Shift_gcn's shift_out transposed,
- * shift_gcn.py:114-118,136), so the following contractions read it without rotation. */
+ * dy_coef as in sgcn_bn_bwd_reduce; per_joint 0 or 3 (see above). */
 int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
                       const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
@@ -332,15 +310,11 @@ int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, in
  * g = dx*(x0 > 0), xhat = (prev_s - prev_mean[c])*prev_invstd[c] — so the previous
  * unit's backward skips its reduce pass. add2_mask (optional, needs add1 and add2): add2
  * enters as add2 * (add2_mask > 0) (a unit's identity-residual gradient dout*(out > 0),
- * formed here rather than written by the unit tail's BatchNorm backward).
- * prev_s_xpos/prev_s_ypos (optional, both or neither, with prev_part): prev_s is the
- * INPUT of the previous unit's stride-1 shift_out, whose output (bn2's input) was never
- * written; each element is re-formed from four taps (as sgcn_bn_bwd_reduce's x_xpos). */
+ * formed here rather than written by the unit tail's BatchNorm backward). */
 int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
                        const float* add2, const float* add2_mask, float* dx, float* dmask_part,
-                       const float* prev_s, const float* prev_s_xpos, const float* prev_s_ypos,
-                       const float* prev_mean, const float* prev_invstd, float* prev_part, int B,
-                       int C, int T, int V, void* stream);
+                       const float* prev_s, const float* prev_mean, const float* prev_invstd,
+                       float* prev_part, int B, int C, int T, int V, void* stream);
 
 /* dmask[u][c] (+)= (sum_b dmask_part[b][c][u]) * (1 - tanh(mask[u][c])^2). */
 int sgcn_mask_grad_finalize(const float* part, const float* mask, int B, int C, int V,

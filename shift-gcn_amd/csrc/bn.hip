@@ -308,19 +308,16 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
 // DYT: the incoming gradient is itself a BatchNorm input-gradient that was never
 // materialised: dy_eff = k1[c]*dy + k2[c]*y + k3[c] with y the tensor read for the ReLU
 // mask (the unit's gcn output H, input of Shift_tcn.bn).
-// ZU (per-joint only): x is the pre-shift_out contraction output; the logical joint v of
-// this thread's column reads it at (v - c) mod V.
-// XSH (per-channel only): x is the stride-1 temporal shift of the given plane (shift
-// positions xsx/xsy) that was never written; each element is re-formed from four taps.
-template <bool PER_JOINT, bool RELU, bool RESBN, bool DYT, bool ZU = false, bool XSH = false>
+// PER_JOINT: x is the Shift_gcn contraction output stored before its shift_out (the
+// per_joint = 3 layout); the logical joint v of this thread's column reads it at
+// (v - c) mod V.
+template <bool PER_JOINT, bool RELU, bool RESBN, bool DYT>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ r, const float* __restrict__ rmean,
     const float* __restrict__ rinvstd, const float* __restrict__ dyc, float2* __restrict__ part,
-    float2* __restrict__ rpart, int C, int T, int V, const float* __restrict__ xsx = nullptr,
-    const float* __restrict__ xsy = nullptr) {
-  static_assert(!XSH || !PER_JOINT, "XSH: per-channel statistics only");
+    float2* __restrict__ rpart, int C, int T, int V) {
   __shared__ float s0[kThreads], s1[kThreads], red[2 * kThreads / 64];
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
@@ -335,12 +332,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const int v = i % V, rr = i / V;
     const int vc = min(v, V - 1);
     const float mu = mean[c * V + vc], is = invstd[c * V + vc];
-    int xd = 0;   // ZU: in-row offset of this column's x element
-    if (ZU) {
-      int vx = v - c % V;
-      vx = vx < 0 ? vx + V : vx;
-      xd = vx - v;
-    }
+    int vx = v - c % V;   // in-row offset of this column's (pre-rotation) x element
+    vx = vx < 0 ? vx + V : vx;
+    const int xd = vx - v;
     if (i < G * V) {
       for (int t0 = rr; t0 < T; t0 += G * kU) {
         float gv[kU], yv[kU], xv[kU], rv[kU];
@@ -376,30 +370,14 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     if (RESBN && i == 0) rpart[plane] = make_float2(b0, b1);
   } else {
     const float mu = mean[c], is = invstd[c];
-    ShiftGeom sg{};
-    if (XSH) sg = shift_geom(xsx[c], xsy[c]);
-    const int dh = kThreads / V, dw = kThreads - (kThreads / V) * V;
     for (int base = 0; base < P; base += kThreads * kU) {
       float gv[kU], yv[kU], xv[kU], rv[kU];
-      int hq = 0, wq = 0;   // XSH: (t, v) of element base + i, advanced by kThreads per u
-      if (XSH) {
-        const int o0 = min(base + i, P - 1);
-        hq = o0 / V;
-        wq = o0 - hq * V;
-      }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int o = min(base + u * kThreads + i, P - 1);
         gv[u] = dy[off + o];
         if (RELU) yv[u] = y[off + o];
-        if (XSH) {
-          xv[u] = shifted_at(x + off, sg, min(hq, T - 1), wq, T, V);
-          hq += dh;
-          wq += dw;
-          if (wq >= V) { wq -= V; ++hq; }
-        } else {
-          xv[u] = x[off + o];
-        }
+        xv[u] = x[off + o];
         if (RESBN) rv[u] = r[off + o];
       }
 #pragma unroll
@@ -630,17 +608,13 @@ __global__ __launch_bounds__(kThreads) void gcn_gather_kernel(const float* __res
 // A2M: add2 enters masked, add2 * (add2m > 0) — the identity-residual gradient of a
 // TCN_GCN_unit, g = dout * (out > 0), formed here instead of being written by the tail's
 // BatchNorm backward.
-// PSH: ps is the previous unit's Shift_tcn.shift_out INPUT (its output, bn2's input, was
-// never written): each s element is re-formed from four taps of that plane with the
-// shift_out positions psx/psy (shifted_at, bit-identical to the stored value).
-template <bool ADD1, bool ADD2, bool PART, bool A2M = false, bool PSH = false>
+template <bool ADD1, bool ADD2, bool PART, bool A2M = false>
 __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
     const float* __restrict__ dxt, const float* __restrict__ x0, const float* __restrict__ m,
     const float* __restrict__ add1, const float* __restrict__ add2, float* __restrict__ dx,
     float* __restrict__ dmask_part, const float* __restrict__ ps,
     const float* __restrict__ pmean, const float* __restrict__ pinvstd,
-    float2* __restrict__ bn_part, int C, int T, int V, const float* __restrict__ add2m,
-    const float* __restrict__ psx = nullptr, const float* __restrict__ psy = nullptr) {
+    float2* __restrict__ bn_part, int C, int T, int V, const float* __restrict__ add2m) {
   // One pass: thread i owns destination joint v' = i % V of rows t = i / V (mod G), so its
   // source joint u = (v' - c) mod V is fixed: one mask value, one dmask accumulator, and
   // the x0 factor of the mask gradient, x0[t, (u + c) mod V] = x0[t, v'], is the element
@@ -657,8 +631,6 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
   const float mu = m[us * C + c];
   float pm = 0.f, pi = 0.f;
   if (PART) { pm = pmean[c]; pi = pinvstd[c]; }
-  ShiftGeom sg{};
-  if (PSH) sg = shift_geom(psx[c], psy[c]);
   float acc = 0.f, b0 = 0.f, b1 = 0.f;
   if (i < G * V) {
     for (int t0 = rr; t0 < T; t0 += G * kU) {
@@ -671,8 +643,7 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
         if (ADD1) a1[k] = add1[off + row + vd];
         if (ADD2) a2[k] = add2[off + row + vd];
         if (A2M) a2q[k] = add2m[off + row + vd];
-        if (PART) sv[k] = PSH ? shifted_at(ps + off, sg, min(t0 + k * G, T - 1), vd, T, V)
-                              : ps[off + row + vd];
+        if (PART) sv[k] = ps[off + row + vd];
       }
 #pragma unroll
       for (int k = 0; k < kU; ++k) {
@@ -760,11 +731,9 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
   if (B == 0) return 0;
   SGCN_REQUIRE(x && part && T > 0);
   hipStream_t st = (hipStream_t)stream;
-  SGCN_REQUIRE(per_joint >= 0 && per_joint <= 3 && per_joint != 2);
+  SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
   if (per_joint == 3)
     moments_kernel<true, true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
-  else if (per_joint)
-    moments_kernel<true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
   else moments_kernel<false><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
   SGCN_LAUNCH_CHECK();
   return 0;
@@ -806,6 +775,7 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
   SGCN_REQUIRE((gather_m == nullptr) == (y_gathered == nullptr));
   SGCN_REQUIRE(!(y_stats && y_gathered) && y_gathered != y);
   SGCN_REQUIRE((rscale == nullptr) == (rshift == nullptr) && (r || !rscale));
+  SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
   hipStream_t st = (hipStream_t)stream;
   const int res = r == nullptr ? 0 : (rscale ? 2 : 1);
   dim3 g(B * C);
@@ -828,8 +798,7 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
     if (res == 0) SGCN_APPLY_ZU(0); else if (res == 1) SGCN_APPLY_ZU(1); else SGCN_APPLY_ZU(2);
 #undef SGCN_APPLY_ZU
   }
-  else if (per_joint) { if (relu) { SGCN_APPLY_R(true, true); } else { SGCN_APPLY_R(true, false); } }
-  else { if (relu) { SGCN_APPLY_R(false, true); } else { SGCN_APPLY_R(false, false); } }
+  else if (relu) { SGCN_APPLY_R(false, true); } else { SGCN_APPLY_R(false, false); }
 #undef SGCN_APPLY_R
 #undef SGCN_APPLY
 #undef SGCN_APPLY_X
@@ -838,26 +807,18 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
 }
 
 int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x,
-                       const float* x_xpos, const float* x_ypos, const float* mean,
-                       const float* invstd, int per_joint, const float* r, const float* rmean,
+                       const float* mean, const float* invstd, int per_joint, const float* r,
+                       const float* rmean,
                        const float* rinvstd, const float* dy_coef, float* part, float* rpart,
                        int B, int C, int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   SGCN_REQUIRE(B > 0 && T > 0 && dy && x && mean && invstd && part && (y || !relu));
   SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE((r == nullptr) == (rpart == nullptr) && (!r || (rmean && rinvstd)));
-  SGCN_REQUIRE((x_xpos == nullptr) == (x_ypos == nullptr));
+  SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
   hipStream_t st = (hipStream_t)stream;
   dim3 g(B * C);
   const bool rb = r != nullptr;
-  if (x_xpos) {   // x = shift(x_given), re-formed per element: the unit-tail form only
-    SGCN_REQUIRE(!per_joint && relu && !r && !dy_coef);
-    bn_bwd_reduce_kernel<false, true, false, false, false, true><<<g, kThreads, 0, st>>>(
-        dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part, (float2*)rpart, C, T,
-        V, x_xpos, x_ypos);
-    SGCN_LAUNCH_CHECK();
-    return 0;
-  }
 #define SGCN_RED(PJ, RL, RB)                                                                \
   (dy_coef ? bn_bwd_reduce_kernel<PJ, RL, RB, true><<<g, kThreads, 0, st>>>(                   \
                  dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
@@ -867,18 +828,7 @@ int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x
                  (float2*)rpart, C, T, V))
   if (per_joint == 3) {   // x = the pre-shift_out contraction output (see the kernel)
     SGCN_REQUIRE(relu);
-#define SGCN_RED_ZU(RB)                                                                       \
-  (dy_coef ? bn_bwd_reduce_kernel<true, true, RB, true, true><<<g, kThreads, 0, st>>>(          \
-                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
-                 (float2*)rpart, C, T, V)                                                     \
-           : bn_bwd_reduce_kernel<true, true, RB, false, true><<<g, kThreads, 0, st>>>(         \
-                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
-                 (float2*)rpart, C, T, V))
-    if (rb) SGCN_RED_ZU(true); else SGCN_RED_ZU(false);
-#undef SGCN_RED_ZU
-  } else if (per_joint) {
-    if (relu) { if (rb) SGCN_RED(true, true, true); else SGCN_RED(true, true, false); }
-    else { if (rb) SGCN_RED(true, false, true); else SGCN_RED(true, false, false); }
+    if (rb) SGCN_RED(true, true, true); else SGCN_RED(true, true, false);
   } else {
     if (relu) { if (rb) SGCN_RED(false, true, true); else SGCN_RED(false, true, false); }
     else { if (rb) SGCN_RED(false, false, true); else SGCN_RED(false, false, false); }
@@ -925,7 +875,7 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
   SGCN_REQUIRE(dy && x && coef && dx && (y || !relu));
   SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE(!rcoef || (r && dr));
-  SGCN_REQUIRE(per_joint >= 0 && per_joint <= 3);
+  SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
   hipStream_t st = (hipStream_t)stream;
   const int res = dr == nullptr ? 0 : (rcoef ? 2 : 1);
   const int F = per_joint ? C * V : C;
@@ -938,9 +888,7 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
 #define SGCN_BA_R(PJ, RL) \
   if (res == 0) SGCN_BA(PJ, RL, 0); else if (res == 1) SGCN_BA(PJ, RL, 1); else SGCN_BA(PJ, RL, 2)
   if (per_joint == 3) { SGCN_REQUIRE(relu); SGCN_BA_R(3, true); }
-  else if (per_joint == 2) { if (relu) { SGCN_BA_R(2, true); } else { SGCN_BA_R(2, false); } }
-  else if (per_joint) { if (relu) { SGCN_BA_R(1, true); } else { SGCN_BA_R(1, false); } }
-  else { if (relu) { SGCN_BA_R(0, true); } else { SGCN_BA_R(0, false); } }
+  else if (relu) { SGCN_BA_R(0, true); } else { SGCN_BA_R(0, false); }
 #undef SGCN_BA_R
 #undef SGCN_BA
   SGCN_LAUNCH_CHECK();
@@ -966,26 +914,19 @@ int sgcn_gcn_gather(const float* x0, const float* m, float* xg, int B, int C, in
 
 int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const float* add1,
                        const float* add2, const float* add2_mask, float* dx, float* dmask_part,
-                       const float* prev_s, const float* prev_s_xpos, const float* prev_s_ypos,
-                       const float* prev_mean, const float* prev_invstd, float* prev_part, int B,
+                       const float* prev_s, const float* prev_mean, const float* prev_invstd,
+                       float* prev_part, int B,
                        int C, int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
   SGCN_REQUIRE(dxt && x0 && m && dx && dmask_part);
   SGCN_REQUIRE(!prev_part || (prev_s && prev_mean && prev_invstd));
   SGCN_REQUIRE(!add2_mask || add2);
-  SGCN_REQUIRE((prev_s_xpos == nullptr) == (prev_s_ypos == nullptr));
-  SGCN_REQUIRE(!prev_s_xpos || prev_part);
   hipStream_t st = (hipStream_t)stream;
   float2* pp = (float2*)prev_part;
-  const bool psh = prev_s_xpos != nullptr;
   if (add2_mask) {   // the identity-unit form: add1 given, add2 masked by add2_mask
     SGCN_REQUIRE(add1);
-    if (pp && psh)
-      gcn_dx_finish_kernel<true, true, true, true, true><<<B * C, kThreads, 0, st>>>(
-          dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,
-          add2_mask, prev_s_xpos, prev_s_ypos);
-    else if (pp)
+    if (pp)
       gcn_dx_finish_kernel<true, true, true, true><<<B * C, kThreads, 0, st>>>(
           dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,
           add2_mask);
@@ -1000,20 +941,14 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
   gcn_dx_finish_kernel<A1, A2, PT><<<B * C, kThreads, 0, st>>>(                           \
       dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,  \
       nullptr)
-#define SGCN_FIN_SH(A1, A2)                                                                 \
-  gcn_dx_finish_kernel<A1, A2, true, false, true><<<B * C, kThreads, 0, st>>>(            \
-      dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,  \
-      nullptr, prev_s_xpos, prev_s_ypos)
 #define SGCN_FIN_P(A1, A2)                                                                  \
   do {                                                                                      \
-    if (pp && psh) SGCN_FIN_SH(A1, A2);                                                     \
-    else if (pp) SGCN_FIN(A1, A2, true);                                                    \
+    if (pp) SGCN_FIN(A1, A2, true);                                                         \
     else SGCN_FIN(A1, A2, false);                                                           \
   } while (0)
   if (add1) { if (add2) SGCN_FIN_P(true, true); else SGCN_FIN_P(true, false); }
   else { if (add2) SGCN_FIN_P(false, true); else SGCN_FIN_P(false, false); }
 #undef SGCN_FIN_P
-#undef SGCN_FIN_SH
 #undef SGCN_FIN
   SGCN_LAUNCH_CHECK();
   return 0;

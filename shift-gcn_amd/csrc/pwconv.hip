@@ -453,7 +453,6 @@ struct DwArgs {
   Plane g;            // A operand rows m: G(b, m, n)
   Plane x;            // B operand rows n: X(b, c, n)
   const float* mask;  // optional mask[v*Nc + c] on X
-  const int* ts;      // TSH: X is the temporal shift of a*X+b (table, Nc x kTsWords)
   float* slab;        // [S][M][Nc]
   float* bslab;       // optional [S][M] row sums of G
   int M, Nc, T, V, B;
@@ -621,10 +620,8 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
 // and RPW = 64/BKP rows per wave instruction; the row offset is a wave-uniform soffset.
 // Positions past the split's end load 0 through the descriptor range.
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int BKP, bool MASK, bool GROT, bool XROT, bool BIAS,
-          bool TSH = false>
+template <int BM, int BN, int WM, int WN, int BKP, bool MASK, bool GROT, bool XROT, bool BIAS>
 __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
-  static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
   constexpr int NT = 64 * WM * WN;
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
   // row pitch: the per-chunk stores put BKP positions x (32/BKP) rows in one 32-lane
@@ -639,7 +636,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
   static_assert(BM % RSTEP == 0 && BN % RSTEP == 0 && 64 % BKP == 0, "bad tile");
   __shared__ float As[2][BKP * AP];
   __shared__ float Bs[2][BKP * BP];
-  __shared__ int ts_s[TSH ? BN * 8 : 1];   // TSH: the tile's channel table (8 words/row)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -674,16 +670,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
   float ra[G_PER], rb[X_PER], rm[MASK ? X_PER : 1], rsum[BIAS ? G_PER : 1];
 #pragma unroll
   for (int i = 0; i < (BIAS ? G_PER : 1); ++i) rsum[i] = 0.f;
-  float rq[TSH ? X_PER : 1][TSH ? 3 : 1];   // TSH: taps q21, q12, q22 (q11 in rb)
-  int tl = 0, vl = 0;                        // TSH: (t, v) of the staged chunk
-  const int v4 = V * 4;
-  if (TSH) {
-    for (int i = tid; i < BN * 8; i += NT) {
-      const int c = min(c0 + i / 8, p.Nc - 1);
-      ts_s[i] = p.ts[c * kTsWords + (i & 7)];
-    }
-    __syncthreads();
-  }
 
   auto load_chunk = [&]() {
     const bool ok = pp < p_end;
@@ -706,25 +692,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
     int cx = v + x_rot0;
     cx = cx >= V ? cx - V : cx;
     const unsigned mcol = (unsigned)((v * p.Nc + rsub) * 4);
-    if (TSH) {
-      // four taps of X around (t + y1, v + x1) per row (see pwg_fwd_kernel); an in-plane
-      // tap never has a negative offset, so the clamps only move taps that are masked
-      // (tap offsets clamped into the row's extent; positions past the split keep the
-      // out-of-range marker: see pwg_fwd_kernel)
-      tl = t;
-      vl = v;
-#pragma unroll
-      for (int i = 0; i < X_PER; ++i) {
-        const int off = ts_s[(rw + rsub + i * RSTEP) * 8];
-        const unsigned so = (unsigned)(c0 + rw + i * RSTEP) * xcs4;
-        const int vo = (int)(xb + lx) + (v + off) * 4, lim = (int)(p.x_bytes - 4u - so);
-        auto tap = [&](int d) { return ok ? (unsigned)min(max(vo + d, 0), lim) : p.x_bytes; };
-        rb[i] = bload(xr, tap(0), so);
-        rq[i][0] = bload(xr, tap(4), so);
-        rq[i][1] = bload(xr, tap(v4), so);
-        rq[i][2] = bload(xr, tap(v4 + 4), so);
-      }
-    } else {
 #pragma unroll
       for (int i = 0; i < X_PER; ++i) {
         const unsigned voff = xb + lx + (unsigned)((XROT ? cx : v) * 4);
@@ -735,7 +702,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
           cx = cx >= V ? cx - V : cx;
         }
       }
-    }
     // advance this lane's position by one chunk
     pp += BKP;
     n += BKP;
@@ -752,18 +718,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
     }
 #pragma unroll
     for (int i = 0; i < X_PER; ++i) {
-      float val = MASK ? rb[i] * rm[i] : rb[i];
-      if (TSH) {
-        const int* pr = ts_s + (rw + rsub + i * RSTEP) * 8;
-        const int tr = tl + pr[1], vr = vl + pr[2];
-        const float a = __int_as_float(pr[5]), bb = __int_as_float(pr[6]);
-        const bool r0 = (unsigned)tr < (unsigned)T, r1 = (unsigned)(tr + 1) < (unsigned)T;
-        const bool q0 = (unsigned)vr < (unsigned)V, q1 = (unsigned)(vr + 1) < (unsigned)V;
-        val = ts_blend(ts_tap(rb[i], a, bb, r0 && q0), ts_tap(rq[i][0], a, bb, r0 && q1),
-                       ts_tap(rq[i][1], a, bb, r1 && q0), ts_tap(rq[i][2], a, bb, r1 && q1),
-                       __int_as_float(pr[3]), __int_as_float(pr[4]));
-      }
-      Bs[buf][kq * BP + rw + rsub + i * RSTEP] = val;
+      Bs[buf][kq * BP + rw + rsub + i * RSTEP] = MASK ? rb[i] * rm[i] : rb[i];
     }
   };
 
@@ -960,15 +915,6 @@ void launch_dw3_t(const DwArgs& a, int S, int tiles, hipStream_t st) {
   dim3 grid(tiles, S);
   const bool mask = a.mask != nullptr, gr = a.g.rsign != 0, xr = a.x.rsign != 0,
              bias = a.bslab != nullptr;
-  if (a.ts) {   // temporal-shift X operand: plain G, no mask / rotation
-    if (bias)
-      pw_dw3_kernel<BM, BN, WM, WN, BKP, false, false, false, true, true>
-          <<<grid, 64 * WM * WN, 0, st>>>(a);
-    else
-      pw_dw3_kernel<BM, BN, WM, WN, BKP, false, false, false, false, true>
-          <<<grid, 64 * WM * WN, 0, st>>>(a);
-    return;
-  }
 #define SGCN_DW3(MS, GR, XR, BI) \
   pw_dw3_kernel<BM, BN, WM, WN, BKP, MS, GR, XR, BI><<<grid, 64 * WM * WN, 0, st>>>(a)
 #define SGCN_DW3_BI(MS, GR, XR) (bias ? SGCN_DW3(MS, GR, XR, true) : SGCN_DW3(MS, GR, XR, false))
@@ -1129,50 +1075,6 @@ size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V) {
   const int tiles = ((M + dw_tile(M) - 1) / dw_tile(M)) * ((Nc + dw_tile(Nc) - 1) / dw_tile(Nc));
   const int S = dw_splits(M, Nc, B, T * V, tiles);
   return (size_t)S * ((size_t)M * Nc + M) * sizeof(float);
-}
-
-size_t sgcn_pw_dw_tshift_ws_bytes(int B, int M, int Nc, int T, int V) {
-  return sgcn_pw_tshift_ws_bytes(Nc) + dw3_ws_bytes(B, M, Nc, T, V);
-}
-
-int sgcn_pw_dw_tshift(const float* g, long long g_bstride, long long g_cstride, const float* x,
-                      long long x_bstride, long long x_cstride, const float* xpos,
-                      const float* ypos, const float* in_scale, const float* in_shift,
-                      float* dw, int dw_transpose, int dw_accumulate, float* dbias,
-                      int dbias_accumulate, void* ws, size_t ws_bytes, int B, int M, int Nc,
-                      int T, int V, void* stream) {
-  SGCN_REQUIRE(B > 0 && M > 0 && Nc > 0 && T > 0 && V > 0 && V < 32768);
-  SGCN_REQUIRE(g && x && dw && ws && xpos && ypos);
-  SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
-  SGCN_REQUIRE(ws_bytes >= sgcn_pw_dw_tshift_ws_bytes(B, M, Nc, T, V));
-  SGCN_REQUIRE(g_cstride * (long long)M < (1LL << 31) && x_cstride * (long long)Nc < (1LL << 31));
-  SGCN_REQUIRE(g_cstride >= (long long)T * V && x_cstride >= (long long)T * V);
-  SGCN_REQUIRE((long long)(B - 1) * g_bstride + (long long)M * g_cstride + (long long)T * V < (1LL << 29));
-  SGCN_REQUIRE((long long)(B - 1) * x_bstride + (long long)Nc * x_cstride + (long long)T * V < (1LL << 29));
-  hipStream_t st = (hipStream_t)stream;
-  int* tab = (int*)ws;
-  float* slab = (float*)((char*)ws + sgcn_pw_tshift_ws_bytes(Nc));
-  tshift_params_kernel<<<(Nc + 63) / 64, 64, 0, st>>>(xpos, ypos, in_scale, in_shift, Nc, V, tab);
-  SGCN_LAUNCH_CHECK();
-  DwArgs a{};
-  a.g = {g, g_bstride, g_cstride, 1, 0};
-  a.x = {x, x_bstride, x_cstride, 1, 0};
-  a.mask = nullptr;
-  a.ts = tab;
-  a.M = M;
-  a.Nc = Nc;
-  a.T = T;
-  a.V = V;
-  a.B = B;
-  a.g_bytes = plane_bytes(g_bstride, g_cstride, 1, B, M, T, V);
-  a.x_bytes = plane_bytes(x_bstride, x_cstride, 1, B, Nc, T, V);
-  a.mask_bytes = 0u;
-  const int S = launch_dw3(a, st, slab, dbias != nullptr);
-  SGCN_LAUNCH_CHECK();
-  launch_slab_reduce(slab, slab + (size_t)S * M * Nc, S, M, Nc, dw, dw_transpose, dw_accumulate,
-                     dbias, dbias_accumulate, st);
-  SGCN_LAUNCH_CHECK();
-  return 0;
 }
 
 int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_tstride,

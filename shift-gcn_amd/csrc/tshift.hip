@@ -197,10 +197,10 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
     float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
     int Hb, int W, int Ho, int add_half) {
   __shared__ float red[2 * kThreads / 64];
-  float bs0 = 0.f, bs1 = 0.f, bmu = 0.f, bis = 0.f;
-  if (BNP) { bmu = bn_mean[blockIdx.x % C]; bis = bn_invstd[blockIdx.x % C]; }
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
+  float bs0 = 0.f, bs1 = 0.f, bmu = 0.f, bis = 0.f;
+  if (BNP) { bmu = bn_mean[c]; bis = bn_invstd[c]; }   // this plane's channel
   const float* __restrict__ go = gout + (size_t)plane * Ho * W;
   const float* __restrict__ src = in + (size_t)plane * Hb * W;
   float* __restrict__ gi = gin + (size_t)plane * Hb * W;
@@ -352,10 +352,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
   __shared__ float red[2 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
-  // out == nullptr (STATS only): the plane moments of the shift output without writing it
-  // (the training unit tail re-forms it from the input: sgcn_tshift_fwd_tail)
-  const bool store = out != nullptr;
-  float* __restrict__ dst = store ? out + (size_t)plane * Ho * W : nullptr;
+  float* __restrict__ dst = out + (size_t)plane * Ho * W;
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];   // shift.py:17-18 (fp32 add)
   const Geom g = make_geom(xpos[c], y);
   float a = 1.f, b = 0.f;
@@ -384,7 +381,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
         const bool ok = own && o < n;
         const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
         v[e] = ok ? val : 0.f;
-        if (store && ok) dst[o] = val;
+        if (ok) dst[o] = val;
       }
     } else {
       Walker pos(base + threadIdx.x, NT, W);
@@ -397,7 +394,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
         const int o = base + e * NT + threadIdx.x;
         const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
         v[e] = o < n ? val : 0.f;
-        if (store && o < n) dst[o] = val;
+        if (o < n) dst[o] = val;
         pos.next();
       }
     }
@@ -567,7 +564,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
 //   {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh} over t where H > 0,
 //   zh = (Z - zmean[c,v]) * zinvstd[c,v]; sgcn_bn_bwd_finalize_gbn combines them.
 template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP, bool GP = false,
-          bool GBN = false, bool SREC = false, bool JA = false>
+          bool GBN = false, bool JA = false>
 __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
@@ -581,7 +578,6 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     float* __restrict__ gzpart = nullptr) {
   static_assert(!GP || STRIDE == 1, "GP is a stride-1 (re-associated) variant");
   static_assert(!GBN || (STRIDE == 1 && BNP && !GP), "GBN: stride-1 shift_in with BNP");
-  static_assert(!SREC || GP, "SREC: bn2's input re-formed in the GP staging");
   // JA (stride 2): both planes staged as in the general path, but the two passes walk
   // their grids on the joint-aligned element stride (NT / W) * W like the stride-1 kernels:
   // a thread's joint w is fixed, so the column part of every tap is a per-thread constant,
@@ -646,25 +642,8 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
         const int i = min(e * NTE + (int)threadIdx.x, nt - 1);
         t[e] = gdy[po + i];
         u1[e] = gy[po + i];
-        if (!SREC) u2[e] = gx[po + i];
+        u2[e] = gx[po + i];
         rin_r[e] = src[min(e * NTE + (int)threadIdx.x, nb - 1)];
-      }
-      if (SREC) {
-        // bn2's input S = shift(in) was never written: the input plane (this thread's own
-        // elements, already in registers) is staged through the LDS and each S element is
-        // re-formed from four taps (shifted_at: bit-identical to the forward's value); the
-        // LDS is then reused for the gradient plane
-        const ShiftGeom sg = shift_geom(x, y);
-        const int w0 = (int)threadIdx.x % W, h0 = (int)threadIdx.x / W, GR = NTE / W;
-#pragma unroll
-        for (int e = 0; e < LPT; ++e) {
-          const int i = e * NTE + threadIdx.x;
-          if (own && i < nb) lds[i] = rin_r[e];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < LPT; ++e) u2[e] = shifted_at(lds, sg, min(h0 + e * GR, Ho - 1), w0, Hb, W);
-        __syncthreads();
       }
 #pragma unroll
       for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
@@ -1050,7 +1029,7 @@ void launch_bwd_lds(bool affine, bool relu, const float* gout, const float* in,
   dim3 grid(B * C), block(NT);
   const size_t lds = (size_t)(STRIDE == 1 ? Ho : H + Ho) * W * sizeof(float);
 #define SGCN_BWDL(A, R, P)                                                                  \
-  tshift_bwd_lds_kernel<NT, LPT, A, R, STRIDE, P, false, false, false, JA>                  \
+  tshift_bwd_lds_kernel<NT, LPT, A, R, STRIDE, P, false, false, JA>                  \
       <<<grid, block, lds, st>>>(gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, \
                                  H, W, Ho, add_half)
   if (bp) {
@@ -1108,10 +1087,8 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
   SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
   const int Ho = H / stride;
   if (B == 0 || Ho == 0) return 0;
-  SGCN_REQUIRE(in && xpos && ypos);
+  SGCN_REQUIRE(in && out && xpos && ypos);
   SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
-  // out == NULL: plane statistics only (LDS-staged planes)
-  SGCN_REQUIRE(out || (plane_stats && H * W <= kFwdLdsMax2));
   hipStream_t st = (hipStream_t)stream;
   const bool aff = in_scale != nullptr, stats = plane_stats != nullptr;
   float2* ps = (float2*)plane_stats;
@@ -1226,25 +1203,18 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
                          int W, int ypos_is_raw, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0);
   SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
-  SGCN_REQUIRE(dy && y && coef && in && xpos && ypos && gin && ws && (gx == nullptr) == (gy == nullptr));
+  SGCN_REQUIRE(dy && y && s && coef && in && xpos && ypos && gin && ws);
+  SGCN_REQUIRE((gx == nullptr) == (gy == nullptr));
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
   SGCN_REQUIRE((long long)B * C < (1LL << 31));
   (void)ypos_is_raw;   // stride 1: the +0.5 of shift.py:17-18 never applies
   hipStream_t st = (hipStream_t)stream;
   float2* pg = (float2*)ws;
   const size_t lds = (size_t)H * W * sizeof(float);
-  // s == NULL: bn2's input is shift(in) itself, re-formed from in's taps (never stored)
 #define SGCN_BNIN(NT, L)                                                                       \
-  do {                                                                                          \
-    if (s)                                                                                      \
-      tshift_bwd_lds_kernel<NT, L, false, true, 1, false, true><<<B * C, NT, lds, st>>>(       \
-          nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, C, H, \
-          W, H, 0, dy, y, s, coef);                                                             \
-    else                                                                                        \
-      tshift_bwd_lds_kernel<NT, L, false, true, 1, false, true, false, true>                    \
-          <<<B * C, NT, lds, st>>>(nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, \
-                                   gin, pg, nullptr, C, H, W, H, 0, dy, y, nullptr, coef);      \
-  } while (0)
+  tshift_bwd_lds_kernel<NT, L, false, true, 1, false, true><<<B * C, NT, lds, st>>>(             \
+      nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, C, H, W, H, \
+      0, dy, y, s, coef)
   const int ntb = H * W <= 4096 ? 256 : 512;
   const int lpb = ra_lpt(H * W, ntb, W);
   SGCN_REQUIRE(lpb > 0);   // W <= 64 and <= 32 elements per thread (caller falls back)

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # same-box A/B of two builds (tuning only, e.g. tools/ab_lib.sh): another in-tree build of
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
-ABI_VERSION = 18
+ABI_VERSION = 19
 EINVAL = -22
 
 _lib = None
@@ -50,9 +50,6 @@ SIGNATURES = {
     "sgcn_pw_fwd_tshift": (_I, [_P, _P, _P, _L, _L, _P, _P, _P, _P, _P, _P, _Z, _P, _L, _L, _I,
                                 _I, _I, _I, _I, _I, _P]),
     "sgcn_pw_dw_ws_bytes": (_Z, [_I, _I, _I, _I, _I]),
-    "sgcn_pw_dw_tshift_ws_bytes": (_Z, [_I, _I, _I, _I, _I]),
-    "sgcn_pw_dw_tshift": (_I, [_P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P, _I, _I, _P, _I, _P,
-                               _Z, _I, _I, _I, _I, _I, _P]),
     "sgcn_pw_dw": (_I, [_P, _L, _L, _I, _I, _P, _L, _L, _I, _I, _P, _P, _I, _I, _P, _I, _P, _Z,
                         _I, _I, _I, _I, _I, _P]),
     "sgcn_moments_ws_bytes": (_Z, [_I, _I, _I, _I]),
@@ -62,15 +59,15 @@ SIGNATURES = {
     "sgcn_bn_eval_coef": (_I, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P]),
     "sgcn_bn_apply": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I,
                            _P]),
-    "sgcn_bn_bwd_reduce": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I,
-                                _I, _I, _I, _P]),
+    "sgcn_bn_bwd_reduce": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I,
+                                _I, _P]),
     "sgcn_bn_bwd_finalize": (_I, [_P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
     "sgcn_bn_bwd_apply": (_I, [_P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I,
                                _P]),
     "sgcn_mask_prep": (_I, [_P, _P, _I, _P]),
     "sgcn_gcn_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
-    "sgcn_gcn_dx_finish": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I,
-                                _I, _I, _P]),
+    "sgcn_gcn_dx_finish": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
+                                _P]),
     "sgcn_tshift_bwd_bnin": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
                                   _I, _I, _P]),
     "sgcn_mask_grad_finalize": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),

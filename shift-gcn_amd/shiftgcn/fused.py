@@ -5,21 +5,20 @@ launches (no torch compute ops), with its backward written out explicitly so tha
 fusions survive training:
 
 Shift_gcn (shift_gcn.py:121-142)
-  fwd : mask_prep -> gcn_gather[shift_in gather * mask, kept for the dW]
-        -> pw_fwd[einsum + bias + shift_out scatter]
-        -> moments(per joint) -> bn_finalize -> [down: pw_fwd -> moments -> finalize]
-        -> bn_apply(+down/identity, ReLU)
-  bwd : bn_bwd_reduce(ReLU mask, both BNs) -> finalize x2 -> bn_bwd_apply[dZ stored
-        gathered: shift_out^T in the store] -> pw_dw(Linear_weight^T, bias)
-        -> pw_fwd(dX in gathered space)
-        -> gcn_dx_finish(shift_in^T + mask, dmask partials) -> mask_grad_finalize
-        -> [down: pw_dw, pw_fwd(accumulate)]
+  fwd : gather[shift_in * mask, written by the previous unit's tail launch]
+        -> pw_fwd[einsum + bias; Z stored before shift_out]
+        -> moments(per joint, shift_out in the addressing) -> bn_finalize
+        -> [down: pw_fwd -> moments -> finalize] -> bn_apply(+down/identity, ReLU)
+  bwd : per-joint BN partials (from the Shift_tcn shift_in backward, or bn_bwd_reduce)
+        -> finalize -> bn_bwd_apply[dZ in Z's layout] -> pw_fwd(dX) -> pw_dw(Linear_weight^T,
+        bias) -> gcn_dx_finish(shift_in^T + mask, dmask partials) -> mask_grad_finalize
+        -> [down: pw_fwd(accumulate), pw_dw]
 Shift_tcn (shift_gcn.py:65-74)
-  fwd : moments -> finalize(bn) -> tshift_fwd[bn affine fused on taps]
-        -> pw_fwd[temporal_linear + bias + ReLU] -> tshift_fwd[stride s, bn2 moments fused]
-        -> finalize(bn2) -> (standalone: bn_apply)
-  bwd : tshift_bwd[ReLU mask fused] -> pw_dw -> pw_fwd(dX)
-        -> tshift_bwd[bn affine + bn-backward partials fused] -> finalize
+  fwd : finalize(bn) -> tshift_fwd[bn affine fused on taps] -> pw_fwd[temporal_linear +
+        bias + ReLU] (C = 256: both in one pw_fwd_tshift) -> tshift_fwd[stride s, bn2
+        moments fused] -> finalize(bn2) -> (standalone: bn_apply)
+  bwd : tshift_bwd[ReLU mask fused; in a unit also bn2's input gradient] -> pw_fwd(dX)
+        -> pw_dw -> tshift_bwd[bn affine + bn-backward partials fused] -> finalize
         -> (standalone: bn_bwd_apply; in a unit the BN input gradient is never written: the
            gcn BN-backward kernels evaluate it on the fly)
 TCN_GCN_unit (shift_gcn.py:160-162): bn2 apply + residual (0 / identity / tcn conv+BN) +
@@ -108,8 +107,6 @@ def _pos_grads(gx, gy, shift):
     allocated here."""
     if not isinstance(gx, ops.PosPartials):
         return gx, gy
-    if not OFF_SMALL:
-        return gx.finalize(torch.empty_like(shift.xpos), torch.empty_like(shift.ypos))
     ox, oy = torch.empty_like(shift.xpos), torch.empty_like(shift.ypos)
     with _OffPath(True, gx.ws):
         gx.finalize(ox, oy)
@@ -127,7 +124,7 @@ def join_side(device):
 # Shift_gcn
 # ======================================================================================
 class GcnSaved:
-    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments", "pj")
+    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
 
 
 def gcn_forward(mod, x0, training, off=False):
@@ -139,7 +136,7 @@ def gcn_forward(mod, x0, training, off=False):
     if mod.has_down:
         conv, bn = mod.down[0], mod.down[1]
         D0 = _empty(B, Cout, T, V, like=x0)
-        down = _OffPath(off and OFF_FWD, x0)
+        down = _OffPath(off, x0)
         with down:
             ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
             if training:
@@ -153,24 +150,20 @@ def gcn_forward(mod, x0, training, off=False):
         m = ops.mask_prep(mod.Feature_Mask)
         xg = ops.gcn_gather(x0, m)    # shift_in gather * mask, once (reused by the dW)
     Z = _empty(B, Cout, T, V, like=x0)
-    # GCN_ZU: Z is stored BEFORE shift_out (plain contraction stores) and the BatchNorm
-    # kernels apply the joint rotation in their addressing (per_joint = 3); else the
-    # contraction's epilogue stores it rotated (per_joint = 1)
-    pj = 3 if GCN_ZU else 1
-    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z, 1, 0 if GCN_ZU else 1),
-               Cout, Cin, T, V)
+    # Z is stored BEFORE shift_out (plain contraction stores) and the BatchNorm kernels
+    # apply the joint rotation in their addressing (per_joint = 3)
+    ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z), Cout, Cin, T, V)
     if training:
-        zst = ops.bn_finalize(ops.moments(Z, pj), B, Cout * V, T, mod.bn, perm_V=V)
+        zst = ops.bn_finalize(ops.moments(Z, 3), B, Cout * V, T, mod.bn, perm_V=V)
     else:
         zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
     if mod.has_down:
         down.wait()
-        H, hm = ops.bn_apply(Z, zst, pj, r=D0, rst=dst, relu=True, out_stats=training)
+        H, hm = ops.bn_apply(Z, zst, 3, r=D0, rst=dst, relu=True, out_stats=training)
     else:
-        H, hm = ops.bn_apply(Z, zst, pj, r=x0, relu=True, out_stats=training)
+        H, hm = ops.bn_apply(Z, zst, 3, r=x0, relu=True, out_stats=training)
     s = GcnSaved()
     s.x0, s.xg, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, xg, Z, zst, D0, dst, H, m
-    s.pj = pj
     s.h_moments = hm   # moments of H for Shift_tcn.bn, produced by the same launch
     return H, s
 
@@ -194,10 +187,10 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     else:
         if mod.has_down:
             conv, bnd = mod.down[0], mod.down[1]
-            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, s.pj, r=s.D0,
+            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, 3, r=s.D0,
                                             rst=s.dst, dy_coef=dy_coef)
         else:
-            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, s.pj, dy_coef=dy_coef)
+            part, rpart = ops.bn_bwd_reduce(dH, s.H, True, s.Z, s.zst, 3, dy_coef=dy_coef)
         coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, Cout * V, B * T,
                                                                    s.zst, mod.bn, perm_V=V)
     dZ = _empty(B, Cout, T, V, like=x0)
@@ -207,25 +200,21 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
         coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
             rpart, B, Cout, B * T * V, s.dst, bnd)
         dD0 = _empty(B, Cout, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2 if s.pj == 1 else 3, r=s.D0,
-                         rcoef=coefD, dr=dD0, dx=dZ, dy_coef=dy_coef)
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 3, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ,
+                         dy_coef=dy_coef)
     else:
         g_id = _empty(B, Cin, T, V, like=x0)
-        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 2 if s.pj == 1 else 3, dr=g_id, dx=dZ,
-                         dy_coef=dy_coef)
-    # dZ is stored gathered (per_joint=2: shift_out transposed by the store), so the
-    # einsum/bias grads and dX read it as a plain plane: G(b,d,n) = dZ[b,d,n]
+        ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 3, dr=g_id, dx=dZ, dy_coef=dy_coef)
+    # dZ is stored in Z's pre-shift_out layout, so the einsum/bias grads and dX read it as
+    # a plain plane: G(b,d,n) = dZ[b,d,n]
     dLW = torch.empty_like(mod.Linear_weight)
     dLb = torch.empty_like(mod.Linear_bias)
     dXt = _empty(B, Cin, T, V, like=x0)
     # on the side stream the weight gradient is enqueued after the dX contraction (it then
     # overlaps the streaming passes that follow instead of competing for the MFMA pipes)
-    if not (off and DW_AFTER_DX):
-        ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
     ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
-    if off and DW_AFTER_DX:
-        with _OffPath(off, dZ, s.xg):
-            ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
+    with _OffPath(off, dZ, s.xg):
+        ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
     g["Linear_weight"], g["Linear_bias"] = dLW, dLb
     a2, a2m = extra_dx if isinstance(extra_dx, tuple) else (extra_dx, None)
     if prev is not None:   # also the previous unit's bn2 backward partials (x0 = its out)
@@ -255,6 +244,12 @@ class TcnSaved:
     __slots__ = ("H", "ast", "As", "R", "S", "sst")
 
 
+def tshift_fused(C):
+    """Whether Shift_tcn's shift_in is formed inside temporal_linear's operand staging
+    (sgcn_pw_fwd_tshift) at C input channels: from TSHIFT_FUSION_MIN_C up."""
+    return C >= TSHIFT_FUSION_MIN_C
+
+
 def gcn_infer_z(mod, x0):
     """Inference Shift_gcn up to its contraction output: (Z, zst, res, res_stats); the
     BN1d + down/identity + ReLU are applied by the consumer (sgcn_tshift_fwd_pre)."""
@@ -276,12 +271,10 @@ def gcn_infer_z(mod, x0):
     return Z, zst, x0, None
 
 
-def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None, s_free=False):
+def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
     """bn -> shift_in -> temporal_linear -> ReLU -> shift_out; returns (S, bn2 stats, saved)
     where S is the shift_out output BEFORE bn2. ``h_moments``: per-plane moments of H
-    already produced by the launch that wrote H (else computed here). ``s_free``
-    (training): S is not written, only its statistics (S = None; the unit tail and the
-    backward re-form it from R)."""
+    already produced by the launch that wrote H (else computed here)."""
     src = H if H is not None else pre[0]
     B, C, T, V = src.shape
     Cout = mod.out_channels
@@ -300,13 +293,10 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None, s_fr
         As = ops.tshift_fwd_pre(pre[0], si.xpos.detach(), si.ypos.detach(), si.stride, pre[1],
                                 pre[2], pre[3], ast)
         ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
-    elif TSHIFT_FUSION and C >= TSHIFT_FUSION_MIN_C:
+    elif tshift_fused(C):
         # shift_in (with Shift_tcn.bn's apply) formed in the contraction's operand staging,
-        # never read back. Mode 1 (default) also stores it from the same registers for the
-        # weight gradient; mode 2 stores nothing and the weight gradient re-forms it from H
-        # (less memory, more VALU in an MFMA-bound kernel: DESIGN.md §Temporal fusion)
-        if TSHIFT_FUSION == 1:
-            As = torch.empty_like(H)
+        # never read back; also stored from the same registers for the weight gradient
+        As = torch.empty_like(H)
         ops.pw_fwd_tshift(tl.weight, tl.bias, PV(H), si.xpos.detach(), si.ypos.detach(), ast,
                           PV(R), Cout, C, T, V, relu=True, x_shifted=As)
     else:
@@ -320,12 +310,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None, s_fr
         return ops.tshift_fwd_tail(R, so.xpos.detach(), so.ypos.detach(), stride, sst,
                                    r=tail[0], rst=tail[1], gather_m=tail[2])
     stats = _empty(B * Cout * 2, like=src) if training else None
-    if s_free:
-        assert training and stride == 1
-        S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats,
-                           store=False)
-    else:
-        S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
+    S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
     if training:
         sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2)
     else:
@@ -359,21 +344,10 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     dWt = torch.empty_like(tl.weight)
     dbt = torch.empty_like(tl.bias)
 
-    def weight_grad():
-        if s.As is None:   # fused forward: re-form the shifted operand from H while staging
-            with _OffPath(off, dRp, H, s.ast.scale):
-                ops.pw_dw_tshift(PV(dRp), PV(H), si.xpos.detach(), si.ypos.detach(), s.ast,
-                                 dWt, Cout, C, T, V, dbias=dbt)
-        else:
-            with _OffPath(off, dRp, s.As):
-                ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
-
-    if not (off and DW_AFTER_DX):
-        weight_grad()
     dAs = _empty(B, C, T, V, like=H)
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
-    if off and DW_AFTER_DX:
-        weight_grad()   # after the dX contraction (see gcn_backward)
+    with _OffPath(off, dRp, s.As):   # after the dX contraction (see gcn_backward)
+        ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
     g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
     # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
     # the Shift_gcn BatchNorm that produced H)
@@ -471,38 +445,24 @@ def unit_forward(unit, x, training):
     # a tiny kernel, made on the side stream off the critical path
     mp = None
     if consumer is not None:
-        mp = _OffPath(off and OFF_SMALL, consumer.Feature_Mask)
+        mp = _OffPath(off, consumer.Feature_Mask)
         with mp:
             gm = ops.mask_prep(consumer.Feature_Mask)
     H, gs = gcn_forward(unit.gcn1, x, training, off=off)
     rs = None
     if unit.residual_kind == "conv":
         # the residual conv branch runs on the side stream, concurrently with Shift_tcn
-        res = _OffPath(off and OFF_FWD, x)
+        res = _OffPath(off, x)
         with res:
             Rc, rst, rs = convbn_core_forward(unit.residual, x, training)
-    so = unit.tcn1.shift_out
-    T, V = H.shape[2], H.shape[3]
-    # S-free tail (training, stride-1 shift_out, no residual conv): bn2's input S is never
-    # written; its statistics come from a moments-only shift pass, the tail launch re-forms
-    # it from R (sgcn_tshift_fwd_tail), and the backward kernels re-form it from R's taps
-    s_free = (S_FREE and training and unit.residual_kind != "conv" and so.stride == 1 and
-              T * V <= ops.TAIL_MAX_PLANE and ops.ra_fits(T * V, V))
-    S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments,
-                                  s_free=s_free)
+    S, sst, ts = tcn_core_forward(unit.tcn1, H, training, h_moments=gs.h_moments)
     # the next unit's Shift_gcn (set by Model.forward_planes for the duration of a call):
     # its gathered, masked input is written by this tail launch too
     if mp is not None:
         mp.wait()
     else:
         gm = None
-    if s_free:
-        out = ops.tshift_fwd_tail(ts.R, so.xpos.detach(), so.ypos.detach(), 1, sst,
-                                  r=x if unit.residual_kind == "identity" else None,
-                                  gather_m=gm)
-        if gm is None:
-            out = out[0]
-    elif unit.residual_kind == "conv":
+    if unit.residual_kind == "conv":
         res.wait()
         out = ops.bn_apply(S, sst, False, r=Rc, rst=rst, relu=True, gather_m=gm)
     elif unit.residual_kind == "identity":
@@ -518,9 +478,7 @@ def unit_forward(unit, x, training):
     # added after) and no gcn down conv (whose dx is accumulated after gcn_dx_finish)
     if (nxt is not None and unit.residual_kind != "conv" and nxt.residual_kind != "conv"
             and not nxt.gcn1.has_down):
-        nxt.__dict__["_prev_tail"] = (
-            out, (S, sst) if S is not None else
-            (ts.R, sst, (so.xpos.detach(), so.ypos.detach())), unit)
+        nxt.__dict__["_prev_tail"] = (out, (S, sst), unit)
     s = UnitSaved()
     s.x, s.gs, s.ts, s.rs, s.out, s.prev = x, gs, ts, rs, out, prev
     s.off = off
@@ -531,7 +489,7 @@ def _gcn_z(unit, s: UnitSaved):
     """(Z, zst) of the unit's Shift_gcn when its BatchNorm's backward sums can come out of
     the shift_in backward launch (no down conv: its BN would need another input)."""
     # (sgcn_tshift_bwd_gbn reads Z in the pre-shift_out layout)
-    return None if unit.gcn1.has_down or s.gs.pj != 3 else (s.gs.Z, s.gs.zst)
+    return None if unit.gcn1.has_down else (s.gs.Z, s.gs.zst)
 
 
 def _off_path_ok(unit, s: UnitSaved):
@@ -563,7 +521,7 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
     ts = s.ts
     S = ts.S
     so = unit.tcn1.shift_out
-    B, Cout, To, V = S.shape if S is not None else ts.R.shape   # S-free: stride 1
+    B, Cout, To, V = S.shape
     kind = unit.residual_kind
     g = {}
     cached = unit.__dict__.pop("_bwd_part", None)
@@ -572,9 +530,6 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
     elif kind == "conv":
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False, r=s.rs.Rc,
                                         rst=s.rs.rst)
-    elif S is None:   # bn2's input re-formed from R's taps
-        part, rpart = ops.bn_bwd_reduce(dout, s.out, True, ts.R, ts.sst, False,
-                                        x_shift=(so.xpos.detach(), so.ypos.detach()))
     else:
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False)
     coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
@@ -596,7 +551,6 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
             s.prev[1].__dict__["_bwd_part"] = (dx, extra["prev_part"])
         g.update({"gcn1." + k: v for k, v in gg.items()})
         return dx, g
-    assert S is not None   # S-free units always take the path above
     dS = torch.empty_like(S)
     dres = None
     if kind == "conv":
@@ -630,32 +584,20 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
 # ======================================================================================
 # autograd Functions (module forward -> Function.apply(module, input, *params))
 # ======================================================================================
-# Shift_tcn's shift_in fused into temporal_linear's operand staging. 1 (default): fused
-# forward that also stores the shifted operand for the weight gradient; 2: nothing stored,
-# the weight gradient re-forms it from H; 0: the round-1 two-launch form (shift launch +
-# contraction). A/B knob: SGCN_TSHIFT_FUSION=0|1|2.
-TSHIFT_FUSION = int(os.environ.get("SGCN_TSHIFT_FUSION", "1"))
-# fuse only from this many channels up (below, the two-launch form is used). With the
-# weight gradients on the side stream, fusing the C = 128 units costs 0.3 % of the step and
-# the C = 256 units are neutral (same-box A/B, profiles/r02_close/ab_tshift_fusion.txt)
+# Shift_tcn's shift_in fused into temporal_linear's operand staging (sgcn_pw_fwd_tshift)
+# from this many input channels up; below, the two-launch form (shift launch + contraction).
+# With the weight gradients on the side stream, fusing the C = 128 units costs 0.3 % of the
+# step and the C = 256 units are neutral (same-box A/B, profiles/r02_close/
+# ab_tshift_fusion.txt). A/B knob (a value above 256 turns the fusion off).
 TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "256"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
 # (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass. A/B knob.
 GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
-# Shift_gcn's shift_out applied by the BatchNorm kernels' addressing (per_joint = 3) instead
-# of by the contraction's rotated epilogue stores. A/B knob.
-GCN_ZU = int(os.environ.get("SGCN_GCN_ZU", "1"))
-# weight-gradient contractions of linked units on a side stream (_OffPath). A/B knob.
+# Off-critical-path launches of linked units on a side stream (_OffPath): the weight-
+# gradient contractions (after the dX contraction of the same operand), the position-
+# gradient finalizes, the next unit's mask and the forward's down / residual conv branches.
+# SGCN_ASYNC_DW=0 serializes everything (bench.py's roofline steps, A/B).
 ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
-# ... with the small off-path kernels too (position-gradient finalize, next unit's mask)
-OFF_SMALL = int(os.environ.get("SGCN_OFF_SMALL", "1"))
-# ... and the forward's down / residual conv branches (A/B knob)
-OFF_FWD = int(os.environ.get("SGCN_OFF_FWD", "1"))
-# ... enqueued after the dX contraction of the same operand (A/B knob)
-DW_AFTER_DX = int(os.environ.get("SGCN_DW_AFTER_DX", "1"))
-# S-free unit tails in training (bn2's input re-formed from R; see unit_forward). A/B knob,
-# off: measured 1.8% slower (measured and rejected).
-S_FREE = int(os.environ.get("SGCN_S_FREE", "0"))
 
 
 def trainable(module):

@@ -117,12 +117,11 @@ def _opt(t, name):
 # temporal shift
 # --------------------------------------------------------------------------------------
 def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=None,
-               ypos_is_raw=True, store=True):
+               ypos_is_raw=True):
     """Forward shift of ``inp`` (B,C,H,W) -> (B,C,H//stride,W). ``ypos`` is the RAW
     parameter (the +0.5 for stride != 1 is applied in-kernel). Optional fused
     per-channel input affine (scale, shift) and per-plane output moments ``stats``
-    (B*C*2 floats). ``store=False`` (with ``stats``): only the moments, nothing written,
-    returns None. float64 tensors run the double-precision kernel (no fused options)."""
+    (B*C*2 floats). float64 tensors run the double-precision kernel (no fused options)."""
     if inp.dtype == torch.float64:
         if scale is not None or shift is not None or stats is not None:
             raise RuntimeError("the fused shift options are float32-only")
@@ -132,13 +131,10 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
     check_input(ypos, "ypos")
     _opt(scale, "scale"), _opt(shift, "shift"), _opt(stats, "stats")
     B, C, H, W = inp.shape
-    if not store:
-        if stats is None or out is not None:
-            raise ValueError("tshift_fwd(store=False) computes the output moments only")
-    elif out is None:
+    if out is None:
         out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
     lib = _lib.load()
-    nb = 4 * (inp.numel() + (out.numel() if store else 0))
+    nb = 4 * (inp.numel() + out.numel())
     with _timed("tshift_fwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_fwd(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos), _ptr(scale),
                                  _ptr(shift), _ptr(stats), B, C, H, W, stride,
@@ -205,10 +201,9 @@ def tshift_fwd_pre(z, xpos, ypos, stride, zst, r, rst, ast):
 
 
 def tshift_fwd_tail(inp, xpos, ypos, stride, st, r=None, rst=None, gather_m=None):
-    """Unit tail: relu(BN(shift(inp)) + res) in one launch with the coefficients of ``st``
-    (eval: running statistics; training: the batch statistics of shift(inp) from
-    tshift_fwd(store=False)), + the next unit's gathered gcn input when ``gather_m`` is
-    given. Returns (out, gathered|None)."""
+    """Inference unit tail: relu(BN(shift(inp)) + res) in one launch with the eval-mode
+    coefficients ``st``, + the next unit's gathered gcn input when ``gather_m`` is given.
+    Returns (out, gathered|None)."""
     check_input(inp, "input")
     if r is not None:
         check_input(r, "residual")
@@ -340,9 +335,10 @@ BNIN_MAX_PLANE = 16384   # sgcn_tshift_bwd_bnin: LDS-staged stride-1 planes only
 
 def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False):
     """Stride-1 shift backward (ReLU mask on ``inp``) whose output gradient is the input
-    gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3, formed in the
-    kernel (``s`` None: s = shift(inp), re-formed from its taps). Returns (grad_input,
-    grad_xpos, grad_ypos)."""
+    gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3 (s = that
+    BatchNorm's input), formed in the kernel. Returns (grad_input, grad_xpos, grad_ypos)."""
+    for t, n in ((dy, "dy"), (y, "y"), (s, "s"), (coef, "coef"), (inp, "input")):
+        check_input(t, n)
     B, C, H, W = inp.shape
     lib = _lib.load()
     dev = inp.device
@@ -350,7 +346,7 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False):
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
     gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
-    nb = 4 * ((2 + (s is not None)) * dy.numel() + 2 * inp.numel())
+    nb = 4 * (3 * dy.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_bwd_bnin(_ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp),
                                       _ptr(xpos), _ptr(ypos), _ptr(gin), _ptr(gx), _ptr(gy),
@@ -491,34 +487,6 @@ def pw_fwd_tshift(w, bias, x: PlaneView, xpos, ypos, st, out: PlaneView, M, K, T
     return out.t
 
 
-def pw_dw_tshift(g: PlaneView, x: PlaneView, xpos, ypos, st, dw, M, Nc, T, V, dbias=None):
-    """Weight/bias gradient of :func:`pw_fwd_tshift`: dW[m][c] = sum G * shift_c(a*x + b)
-    (sgcn_pw_dw_tshift, the shifted operand re-formed from x while staging)."""
-    check_input(dw, "dw")
-    _opt(dbias, "dbias")
-    if x.tstride != 1 or x.rsign != 0 or g.tstride != 1 or g.rsign != 0:
-        raise ValueError("pw_dw_tshift: plain planes only")
-    B = g.t.shape[0]
-    lib = _lib.load()
-    bc = _batch_chunk([(g, M), (x, Nc)], B, T, V)
-    nbytes = lib.sgcn_pw_dw_tshift_ws_bytes(bc, M, Nc, T, V)
-    ws = torch.empty((nbytes + 3) // 4, device=g.t.device, dtype=_F32)
-    P = B * T * V
-    sc = st.scale if st is not None else None
-    sh = st.shift if st is not None else None
-    with _timed("pw_dw", 2.0 * P * M * Nc, 4.0 * P * (M + Nc), g.t, f"TSH M{M} N{Nc} T{T} V{V}"):
-        for b0 in range(0, B, bc):
-            nb = min(bc, B - b0)
-            first = b0 == 0
-            rc = lib.sgcn_pw_dw_tshift(g.t.data_ptr() + 4 * b0 * g.bstride, g.bstride, g.cstride,
-                                       x.t.data_ptr() + 4 * b0 * x.bstride, x.bstride, x.cstride,
-                                       _ptr(xpos), _ptr(ypos), _ptr(sc), _ptr(sh), _ptr(dw), 0,
-                                       int(not first), _ptr(dbias), int(not first), _ptr(ws),
-                                       nbytes, nb, M, Nc, T, V, _stream(g.t))
-            _lib.check(rc, "sgcn_pw_dw_tshift")
-    return dw
-
-
 # --------------------------------------------------------------------------------------
 # BatchNorm / unit tails
 # --------------------------------------------------------------------------------------
@@ -604,20 +572,16 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
 
 
 def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats = None,
-                  dy_coef=None, x_shift=None):
-    """``x_shift`` = (xpos, ypos): the BatchNorm input is the stride-1 temporal shift of
-    ``x`` with these positions (never written), re-formed per element."""
+                  dy_coef=None):
     check_input(dy, "grad_output")
     B, C, T, V = x.shape
-    xsx, xsy = x_shift if x_shift is not None else (None, None)
     dev = x.device
     part = torch.empty((B * C * (V if per_joint else 1) * 2,), device=dev, dtype=_F32)
     rpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if r is not None else None
     nb = 4 * x.numel() * (2 + (y is not None) + (r is not None))
     with _timed("bn_bwd_reduce", 0, nb, x, _shp(x)):
-        rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(xsx),
-                                            _ptr(xsy), _ptr(st.mean), _ptr(st.invstd),
-                                            int(per_joint),
+        rc = _lib.load().sgcn_bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu), _ptr(x),
+                                            _ptr(st.mean), _ptr(st.invstd), int(per_joint),
                                             _ptr(r), _ptr(rst.mean) if rst else None,
                                             _ptr(rst.invstd) if rst else None, _ptr(dy_coef),
                                             _ptr(part), _ptr(rpart), B, C, T, V, _stream(x))
@@ -693,20 +657,17 @@ def gcn_gather(x0, m):
 
 def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
     """Returns (dx, dmask partials[, prev_part]); ``prev`` = (S, BnStats) of the previous
-    unit's bn2 adds its backward-reduce partials (see sgcn_gcn_dx_finish), or
-    (R, BnStats, (xpos, ypos)) when bn2's input S = shift(R) was never written."""
+    unit's bn2 adds its backward-reduce partials (see sgcn_gcn_dx_finish)."""
     B, C, T, V = dxt.shape
     dx = torch.empty_like(dxt)
     part = torch.empty((B * C * V,), device=dxt.device, dtype=_F32)
     pp = torch.empty((B * C * 2,), device=dxt.device, dtype=_F32) if prev is not None else None
-    ps, pst = prev[:2] if prev is not None else (None, None)
-    psx, psy = prev[2] if prev is not None and len(prev) > 2 else (None, None)
+    ps, pst = prev if prev is not None else (None, None)
     nb = 4 * dxt.numel() * (3 + sum(t is not None for t in (add1, add2, add2_mask, ps)))
     with _timed("gcn_dx_finish", 0, nb, dxt, _shp(dxt)):
         rc = _lib.load().sgcn_gcn_dx_finish(_ptr(dxt), _ptr(x0), _ptr(m), _ptr(add1),
                                             _ptr(add2), _ptr(add2_mask), _ptr(dx), _ptr(part),
-                                            _ptr(ps), _ptr(psx), _ptr(psy),
-                                            _ptr(pst.mean) if pst else None,
+                                            _ptr(ps), _ptr(pst.mean) if pst else None,
                                             _ptr(pst.invstd) if pst else None, _ptr(pp), B, C,
                                             T, V, _stream(dxt))
     _lib.check(rc, "sgcn_gcn_dx_finish")

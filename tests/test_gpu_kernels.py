@@ -141,12 +141,24 @@ def test_pw_dw_large_split_is_deterministic():
     torch.testing.assert_close(a.double(), ref, rtol=1e-5, atol=2e-3)
 
 
+def _rot(zu):
+    """logical z[c, t, w] = zu[c, t, (w - c) mod V] (Shift_gcn's shift_out,
+    shift_gcn.py:114-118,136)"""
+    B, C, T, V = zu.shape
+    idx = (torch.arange(V, device=zu.device)[None, :] - torch.arange(C, device=zu.device)[:, None]) % V
+    return zu.gather(3, idx.view(1, C, 1, V).expand(B, C, T, V))
+
+
 @pytest.mark.parametrize("per_joint", [False, True])
 def test_bn_train_forward_backward_matches_torch(per_joint):
+    """per_joint: Shift_gcn.bn (BatchNorm1d over (b, t) of (v, c) features) on the
+    contraction output stored before its shift_out (per_joint = 3: the kernels read x at
+    the pre-rotation position and store dx there); else BatchNorm2d."""
     from shiftgcn import ops
     torch.manual_seed(1)
     B, C, T, V = 6, 16, 20, 25
-    x = torch.randn(B, C, T, V, device=DEV) * 2 + 0.7
+    xu = torch.randn(B, C, T, V, device=DEV) * 2 + 0.7    # as stored (pre-rotation)
+    x = _rot(xu) if per_joint else xu                    # the BatchNorm's logical input
     r = torch.randn(B, C, T, V, device=DEV)
     F = C * V if per_joint else C
     bn = torch.nn.BatchNorm1d(F).to(DEV) if per_joint else torch.nn.BatchNorm2d(C).to(DEV)
@@ -157,10 +169,11 @@ def test_bn_train_forward_backward_matches_torch(per_joint):
     bn_ref = type(bn)(F).to(DEV); bn_ref.load_state_dict(bn.state_dict())
     bnr_ref = torch.nn.BatchNorm2d(C).to(DEV); bnr_ref.load_state_dict(bnr.state_dict())
     perm = V if per_joint else 0
-    part = ops.moments(x, per_joint)
+    pj = 3 if per_joint else 0
+    part = ops.moments(xu, pj)
     st = ops.bn_finalize(part, B, F, T if per_joint else T * V, bn, perm_V=perm)
     rst = ops.bn_finalize(ops.moments(r, False), B, C, T * V, bnr)
-    y = ops.bn_apply(x, st, per_joint, r=r, rst=rst, relu=True)
+    y = ops.bn_apply(xu, st, pj, r=r, rst=rst, relu=True)
 
     def ref_bn(mod, t, pj):
         if pj:  # BatchNorm1d over (b,t) of features (v, c) -> reference feature v*C + c
@@ -177,13 +190,13 @@ def test_bn_train_forward_backward_matches_torch(per_joint):
     assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
     dy = torch.randn_like(y)
     yr.backward(dy)
-    p, rp = ops.bn_bwd_reduce(dy, y, True, x, st, per_joint, r=r, rst=rst)
+    p, rp = ops.bn_bwd_reduce(dy, y, True, xu, st, pj, r=r, rst=rst)
     coef, dg, db = ops.bn_bwd_finalize(p, B, F, B * (T if per_joint else T * V), st, bn,
                                        perm_V=perm)
     rcoef, rdg, rdb = ops.bn_bwd_finalize(rp, B, C, B * T * V, rst, bnr)
     dr = torch.empty_like(r)
-    dx = ops.bn_bwd_apply(dy, y, True, x, coef, per_joint, r=r, rcoef=rcoef, dr=dr)
-    torch.testing.assert_close(dx, xr.grad, rtol=1e-4, atol=1e-5)
+    dx = ops.bn_bwd_apply(dy, y, True, xu, coef, pj, r=r, rcoef=rcoef, dr=dr)
+    torch.testing.assert_close(_rot(dx) if per_joint else dx, xr.grad, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dr, rr.grad, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dg, bn_ref.weight.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(db, bn_ref.bias.grad, rtol=1e-4, atol=1e-4)

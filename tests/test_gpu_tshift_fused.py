@@ -5,11 +5,9 @@ model/shift_gcn.py:66-69, shift_cuda_kernel.cu:11-76).
 * forward: ``sgcn_pw_fwd_tshift`` == ``sgcn_tshift_fwd`` (bn affine on the taps) followed
   by ``sgcn_pw_fwd``, bit for bit (same tap arithmetic, same K order), including planes
   whose position count is not a tile multiple, |ypos| > 1, x shifts of a whole joint, V=33;
-* weight gradient: ``sgcn_pw_dw_tshift`` == ``sgcn_pw_dw`` on the materialised shifted
-  tensor (bit for bit where both use the same split-K kernel, else within 1e-6 relative);
-* the side output (mode 1, default) is the shifted operand, element for element;
-* every fusion mode (0: two launches, 1: fused + side output, 2: the weight gradient re-forms
-  the operand) gives the same unit parity vs the oracle;
+* the side output is the shifted operand, element for element (the weight gradient's
+  operand, read by ``sgcn_pw_dw``);
+* the fused form and the two-launch form give the same unit parity vs the oracle;
 * in a training step there is no separate shift_in launch for the units at or above the
   channel threshold: the other temporal-shift forward launches are the 10 shift_outs
   (whose output feeds bn2's statistics).
@@ -72,48 +70,24 @@ def test_fused_forward_bit_identical_to_two_launch(case):
     assert torch.equal(xs, As)        # the side output is the shifted operand, every element
 
 
-@pytest.mark.parametrize("case", CASES, ids=["x".join(map(str, c)) for c in CASES])
-def test_fused_weight_gradient_matches_materialised(case):
-    from shiftgcn import ops
-    from shiftgcn.ops import PlaneView as PV
-    B, K, M, T, V = case
-    h, w, bias, xpos, ypos, scale, shift = _inputs(*case, seed=3 * sum(case))
-    gr = torch.randn(B, M, T, V, device=DEV)
-    As = ops.tshift_fwd(h, xpos, ypos, 1, scale=scale, shift=shift)
-    dw1 = torch.empty(M, K, device=DEV)
-    db1 = torch.empty(M, device=DEV)
-    ops.pw_dw(PV(gr), PV(As), dw1, M, K, T, V, dbias=db1)
-    dw2 = torch.empty(M, K, device=DEV)
-    db2 = torch.empty(M, device=DEV)
-    ops.pw_dw_tshift(PV(gr), PV(h), xpos, ypos, _St(scale, shift), dw2, M, K, T, V, dbias=db2)
-    # fp64 reference of the same contraction on the materialised operand
-    ref = torch.einsum("bmn,bkn->mk", gr.double().flatten(2), As.double().flatten(2))
-    torch.cuda.synchronize()
-    assert float((dw2.double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
-    assert float((dw2 - dw1).abs().max()) <= 1e-6 * float(dw1.abs().max()) + 1e-7
-    assert float((db2 - db1).abs().max()) <= 1e-6 * float(db1.abs().max()) + 1e-7
-
-
-@pytest.mark.parametrize("mode", [0, 1, 2])
-def test_unit_matches_oracle_in_every_fusion_mode(monkeypatch, mode):
-    """SGCN_TSHIFT_FUSION 0 (two launches), 1 (fused, shifted operand stored) and 2 (weight
-    gradient re-forms the operand) give the same unit parity, with the channel threshold
-    at 0 so the C = 128 unit below takes the fused form."""
+@pytest.mark.parametrize("min_c", [0, 1024])
+def test_unit_matches_oracle_fused_and_two_launch(monkeypatch, min_c):
+    """The fused shift_in contraction (threshold 0: the C = 128 unit below takes it) and the
+    two-launch form (threshold above every width) give the same unit parity."""
     import formula
     import shiftgcn
     from oracle import model_oracle as mo
     from shiftgcn import fused
     from test_gpu_blocks import _compare
-    monkeypatch.setattr(fused, "TSHIFT_FUSION", mode)
-    monkeypatch.setattr(fused, "TSHIFT_FUSION_MIN_C", 0)
+    monkeypatch.setattr(fused, "TSHIFT_FUSION_MIN_C", min_c)
     ref = mo.TCN_GCN_unit(64, 128, None, stride=2, num_point=25)
-    formula.fill_state(ref, seed=mode + 17)
+    formula.fill_state(ref, seed=min_c + 17)
     ours = shiftgcn.TCN_GCN_unit(64, 128, None, stride=2, num_point=25).to(DEV)
     ours.load_state_dict(ref.state_dict())
     ref.train()
     ours.train()
-    x = formula.tensor((3, 64, 18, 25), 50 + mode, 1.0)
-    g = formula.tensor((3, 128, 9, 25), 60 + mode, 1.0)
+    x = formula.tensor((3, 64, 18, 25), 50 + min_c, 1.0)
+    g = formula.tensor((3, 128, 9, 25), 60 + min_c, 1.0)
     xr = x.clone().requires_grad_(True)
     yr = ref(xr)
     yr.backward(g)
@@ -121,7 +95,7 @@ def test_unit_matches_oracle_in_every_fusion_mode(monkeypatch, mode):
     yo = ours(xo)
     yo.backward(g.to(DEV))
     torch.cuda.synchronize()
-    _compare(ref, ours, xr, yr, xo, yo, f"mode{mode}")
+    _compare(ref, ours, xr, yr, xo, yo, f"min_c{min_c}")
 
 
 @pytest.mark.parametrize("min_c", [0, None])
@@ -131,7 +105,6 @@ def test_training_step_has_no_shift_in_launch(monkeypatch, min_c):
     import formula
     import shiftgcn
     from shiftgcn import fused, ops
-    assert fused.TSHIFT_FUSION
     if min_c is not None:
         monkeypatch.setattr(fused, "TSHIFT_FUSION_MIN_C", min_c)
     calls = {"affine": 0, "plain": 0}

@@ -6,6 +6,6 @@ cd $ROOT
 mkdir -p gpurun_out/ab
 for c in ${CASES:-1:0 0:0 1:128}; do
   m=${c%%:*}; k=${c##*:}
-  SGCN_TSHIFT_FUSION=$m SGCN_TSHIFT_FUSION_MIN_C=$k timeout -k 10 300 python -u bench.py --cpu-baseline 0 ${BENCH_ARGS} > gpurun_out/ab/bench_m${m}_k${k}.log 2>&1
+  SGCN_TSHIFT_FUSION_MIN_C=$k timeout -k 10 300 python -u bench.py --cpu-baseline 0 ${BENCH_ARGS} > gpurun_out/ab/bench_m${m}_k${k}.log 2>&1
   echo "mode $m minC $k: $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab/bench_m${m}_k${k}.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['step_breakdown_ms'])")"
 done
