@@ -268,9 +268,24 @@ def gen_models(ref_sg, out):
         out[f"model_{name}_logits_train64"] = _np(logits64)
         p64 = dict(m64.named_parameters())
         out[f"model_{name}_grad_norm64"] = np.array([float(p64[n].grad.norm()) for n in names])
+        out[f"model_{name}_grad_sum64"] = np.array([float(p64[n].grad.sum()) for n in names])
         for n in names:
             if n.endswith(("xpos", "ypos")):
                 out[f"model_{name}_grad64.{n}"] = _np(p64[n].grad)
+        # ... and its SGD step: the fp32 step's own deviation from it (per parameter sum)
+        # is the bar the HIP step is held to (tests/test_train_step.py)
+        groups64 = []
+        for key, value in m64.named_parameters():
+            wd = 1e-4
+            if "Linear_weight" in key:
+                wd = 1e-3
+            elif "Mask" in key:
+                wd = 0.0
+            groups64.append({"params": value, "lr": 0.1, "weight_decay": wd})
+        torch.optim.SGD(groups64, momentum=0.9, nesterov=True).step()
+        out[f"model_{name}_step_param_sum64"] = np.array(
+            [float(p.detach().sum()) for pn, p in m64.named_parameters()
+             if p.dtype.is_floating_point])
 
 
 def main():

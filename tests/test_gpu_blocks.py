@@ -178,14 +178,26 @@ def test_model_matches_golden_fixture(golden, case):
     m = m.to(DEV)
     x, labels = model_case_inputs(*case)
     m.eval()
-    with torch.no_grad():
-        _rel_close(m(x.to(DEV)).cpu(), fx[f"model_{name}_logits_eval"], 1e-4, "eval logits")
+    with torch.no_grad():   # running-statistics BatchNorms: well conditioned
+        _rel_close(m(x.to(DEV)).cpu(), fx[f"model_{name}_logits_eval"], 1e-5, "eval logits")
     m.train()
     logits = m(x.to(DEV))
     loss = torch.nn.functional.cross_entropy(logits, labels.to(DEV))
     loss.backward()
-    _rel_close(logits.detach().cpu(), fx[f"model_{name}_logits_train"], 1e-4, "train logits")
-    assert abs(float(loss) - float(fx[f"model_{name}_loss"])) < 1e-4 * max(1, float(loss))
+    # train-mode logits and loss: no further from the reference's float64 run than 2x its
+    # own fp32 run is (1e-5 floor), the bar the gradients are held to below
+    l64 = torch.from_numpy(fx[f"model_{name}_logits_train64"]).double()
+    l32 = torch.from_numpy(fx[f"model_{name}_logits_train"]).double()
+    lo = logits.detach().cpu().double()
+    sc = float(l64.abs().max())
+    el_o, el_r = float((lo - l64).abs().max()) / sc, float((l32 - l64).abs().max()) / sc
+    loss64 = float(torch.nn.functional.cross_entropy(l64, labels))
+    ls_o = abs(float(loss) - loss64) / max(1.0, loss64)
+    ls_r = abs(float(fx[f"model_{name}_loss"]) - loss64) / max(1.0, loss64)
+    print(f"\n[{name} bs=2] train logits rel err vs fp64: HIP {el_o:.2e}, reference fp32 "
+          f"{el_r:.2e}; loss {ls_o:.2e} vs {ls_r:.2e}")
+    assert el_o <= max(2 * el_r, 1e-5), (el_o, el_r)
+    assert ls_o <= max(2 * ls_r, 1e-5), (ls_o, ls_r)
     names = list(fx[f"model_{name}_grad_names"])
     params = dict(m.named_parameters())
     gnorm = np.array([float(params[n].grad.double().norm()) for n in names])
@@ -204,7 +216,6 @@ def test_model_matches_golden_fixture(golden, case):
                                                                    np.median(err_ref))
     assert err_ours.max() <= 2 * err_ref.max(), (err_ours.max(), err_ref.max())
     assert np.all(gnorm[zero] < 1e-3)
-    _rel_close(logits.detach().cpu(), fx[f"model_{name}_logits_train64"], 1e-4, "vs fp64")
     flips_ours = flips_ref = 0
     for n in names:
         if n.endswith("ypos"):

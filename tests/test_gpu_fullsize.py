@@ -5,12 +5,15 @@ fixtures) is run on the GPU with the torch-gather temporal shift of ``oracle/tor
 in place of ``shift_cuda`` (BASELINE config 1's "naive torch.gather fallback"), in fp32
 and in fp64, beside the HIP path:
 
-* config 2: one NTU training step at bs=64, x = (64, 3, 300, 25, 2): logits and loss within
-  1e-4, gradient norms at least as close to the fp64 eager result as the fp32 eager result
-  is (2x margin; model-level fp32 gradients through 10 train-mode BatchNorm units are
-  ill-conditioned), ypos sign flips vs fp64 no more than 2x the fp32 eager's + 2, BN
-  running statistics within 1e-4. At this size the split-K weight gradients, the 32-bit
-  buffer offsets and the plane-size kernel switches all engage.
+* config 2 (NTU, x = (64, 3, 300, 25, 2)) and config 3 (MediaPipe, x = (64, 3, 300, 33, 1)):
+  one training step at bs=64 each. Every quantity is held to the same relative bar: no
+  further from the fp64 eager result than 2x the fp32 eager result is — logits (max abs
+  error over max |logit|) and loss with a 1e-5 floor, gradients in norm per parameter
+  (median and max over parameters; model-level fp32 gradients through 10 train-mode
+  BatchNorm units are ill-conditioned), ypos sign flips vs fp64 2x the fp32 eager's + 2;
+  BN running statistics within 1e-4. The achieved errors are printed. At these sizes the
+  split-K weight gradients, the 32-bit buffer offsets and the plane-size kernel switches
+  (V = 25 and V = 33: 7,500- and 9,900-float planes, 256- vs 512-thread kernels) engage.
 * config 4: one 4-stream MediaPipe ensemble batch at bs=256 windows (eval mode): fused
   float64 logits within 1e-4 and fall scores within 1e-5 of the fp64 eager ensemble.
 * beyond the 2^29-element operand limit of the contraction kernels (NTU at > ~279 clips
@@ -35,11 +38,21 @@ def eager_gpu_shift(monkeypatch):
     monkeypatch.setattr(mo.Shift, "function", ts.TorchShiftFunction)
 
 
-def _ntu_inputs(bs):
+# BASELINE configs 2 and 3: (num_class, V, M, graph)
+CONFIGS = {"ntu": (60, 25, 2, "graph.ntu_rgb_d.Graph"),
+           "mp": (2, 33, 1, "graph.mediapipe_pose.Graph")}
+
+
+def _inputs(cfg, bs):
+    num_class, V, M, _ = CONFIGS[cfg]
     g = torch.Generator().manual_seed(1000)
-    x = torch.randn(bs, 3, 300, 25, 2, generator=g)
-    labels = torch.randint(0, 60, (bs,), generator=g)
+    x = torch.randn(bs, 3, 300, V, M, generator=g)
+    labels = torch.randint(0, num_class, (bs,), generator=g)
     return x, labels
+
+
+def _ntu_inputs(bs):
+    return _inputs("ntu", bs)
 
 
 def _run_train(model, x, labels):
@@ -55,19 +68,21 @@ def _run_train(model, x, labels):
     return logits.detach().double().cpu(), float(loss), grads, bufs
 
 
-def test_config2_ntu_bs64_train_step_matches_eager_reference(eager_gpu_shift):
+@pytest.mark.parametrize("cfg", ["ntu", "mp"])
+def test_config2_3_bs64_train_step_matches_eager_reference(eager_gpu_shift, cfg):
     import shiftgcn
-    x, labels = _ntu_inputs(64)
+    num_class, V, M, graph = CONFIGS[cfg]
+    x, labels = _inputs(cfg, 64)
     torch.manual_seed(1)
-    ours = shiftgcn.Model(num_class=60, num_point=25, num_person=2,
-                          graph="graph.ntu_rgb_d.Graph").to(DEV).train()
+    ours = shiftgcn.Model(num_class=num_class, num_point=V, num_person=M,
+                          graph=graph).to(DEV).train()
     state = {k: v.detach().cpu().clone() for k, v in ours.state_dict().items()}
     lo, losso, go, bo = _run_train(ours, x.to(DEV), labels.to(DEV))
     del ours
     torch.cuda.empty_cache()
     res = {}
     for dt in (torch.float32, torch.float64):
-        ref = mo.Model(num_class=60, num_point=25, num_person=2)
+        ref = mo.Model(num_class=num_class, num_point=V, num_person=M)
         ref.load_state_dict(state)
         ref = ref.to(DEV, dt).train()
         res[dt] = _run_train(ref, x.to(DEV, dt), labels.to(DEV))
@@ -77,8 +92,13 @@ def test_config2_ntu_bs64_train_step_matches_eager_reference(eager_gpu_shift):
     l64, loss64, g64, b64 = res[torch.float64]
 
     scale = float(l64.abs().max())
-    assert float((lo - l64).abs().max()) <= 1e-4 * scale
-    assert abs(losso - loss64) <= 1e-4 * max(1.0, abs(loss64))
+    el_o, el_r = float((lo - l64).abs().max()) / scale, float((l32 - l64).abs().max()) / scale
+    ls_o = abs(losso - loss64) / max(1.0, abs(loss64))
+    ls_r = abs(loss32 - loss64) / max(1.0, abs(loss64))
+    print(f"\n[{cfg}] logits rel err vs fp64: HIP {el_o:.2e}, fp32 eager {el_r:.2e}; "
+          f"loss: HIP {ls_o:.2e}, fp32 eager {ls_r:.2e}")
+    assert el_o <= max(2 * el_r, 1e-5), (el_o, el_r)
+    assert ls_o <= max(2 * ls_r, 1e-5), (ls_o, ls_r)
     for k, b in b64.items():
         err = float((bo[k] - b).abs().max())
         assert err <= 1e-4 * float(b.abs().max()) + 1e-6, (k, err)
@@ -100,6 +120,9 @@ def test_config2_ntu_bs64_train_step_matches_eager_reference(eager_gpu_shift):
         err_o.append(float((go[k] - g64[k]).norm()) / n64)
         err_r.append(float((g32[k] - g64[k]).norm()) / n64)
     err_o, err_r = np.array(err_o), np.array(err_r)
+    print(f"[{cfg}] grad rel err vs fp64 (median / max over params): HIP "
+          f"{np.median(err_o):.2e} / {err_o.max():.2e}, fp32 eager {np.median(err_r):.2e} / "
+          f"{err_r.max():.2e}; ypos sign flips {flips_o} vs {flips_r}")
     assert np.median(err_o) <= 2 * np.median(err_r) + 1e-5, (np.median(err_o), np.median(err_r))
     assert err_o.max() <= 2 * err_r.max() + 1e-5, (err_o.max(), err_r.max())
     assert flips_o <= 2 * flips_r + 2, (flips_o, flips_r)
