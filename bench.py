@@ -49,6 +49,7 @@ PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # per-config PMC files (the NTU figures must never be quoted on another workload)
 PMC_TRAFFIC_BY_CONFIG = {"ntu": PMC_TRAFFIC,
                          "mp": os.path.join(REPO, "profiles", "pmc_traffic_mp.json")}
+PMC_TRAFFIC_ENS = os.path.join(REPO, "profiles", "pmc_traffic_ens.json")
 
 
 def pmc_traffic(op, path=None):
@@ -58,6 +59,40 @@ def pmc_traffic(op, path=None):
         return d["ops"][op]["bytes_per_call"], d.get("source", "")
     except (OSError, KeyError, ValueError):
         return None, ""
+
+
+def pmc_ops(path):
+    try:
+        with open(path) as f:
+            return json.load(f).get("ops", {})
+    except (OSError, ValueError):
+        return {}
+
+
+def class_rates(summ, n_iters, pmc=None):
+    """Per op class: ms per step and the achieved rate against its own bound — TF/s of
+    algorithmic FLOP vs the FP32 MFMA peak for the contractions, GB/s of algorithmic bytes
+    vs the HBM peak for the streaming passes (SURVEY §8d per-kernel definitions) — plus the
+    HBM bytes per step the committed PMC passes measured for the class, when present."""
+    out = {}
+    for k, v in sorted(summ.items()):
+        sec = v["ms_total"] / 1e3
+        e = {"ms": round(v["ms_total"] / n_iters, 3), "launches": v["launches"] // n_iters}
+        gbs = v["bytes"] / sec / 1e9 if sec > 0 else 0.0
+        if v["flops"] > 0:
+            tf = v["flops"] / sec / 1e12 if sec > 0 else 0.0
+            e.update(bound="mfma", tflops=round(tf, 2), frac=round(tf / PEAK_FP32_TFLOPS, 4),
+                     gbs_algorithmic=round(gbs, 1))
+        else:
+            e.update(bound="hbm", gbs=round(gbs, 1), frac=round(gbs / PEAK_HBM_GBS, 4))
+        e["algorithmic_mb_per_step"] = round(v["bytes"] / n_iters / 1e6, 1)
+        t = (pmc or {}).get(k, {})
+        if "bytes_per_step" in t:
+            e["pmc_mb_per_step"] = round(t["bytes_per_step"] / 1e6, 1)
+            if v["bytes"] > 0:
+                e["pmc_over_algorithmic"] = round(t["bytes_per_step"] / (v["bytes"] / n_iters), 3)
+        out[k] = e
+    return out
 
 
 def parse():
@@ -330,6 +365,8 @@ def main():
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
                 "step_breakdown_ms": {k: round(v["ms_total"] / n_meas, 3)
                                       for k, v in sorted(summ.items())},
+                "class_rates": class_rates(
+                    summ, n_meas, pmc_ops(PMC_TRAFFIC_BY_CONFIG.get(args.config, ""))),
                 # HIP events around every C-ABI launch vs events around the whole step (same
                 # steps): the rest is torch's head/loss/optimizer kernels and launch gaps
                 "step_ms_event_timed": round(step_ms_meas, 3),
@@ -397,6 +434,7 @@ def _roofline(summ, n_iters, value_per_gpu, gflop_per_unit):
             "avg_launch_us": round(per_launch_s * 1e6, 2),
             "iter_breakdown_ms": {k: round(v["ms_total"] / n_iters, 3)
                                   for k, v in sorted(summ.items())},
+            "class_rates": class_rates(summ, n_iters, pmc_ops(PMC_TRAFFIC_ENS)),
             "whole_iter_frac_of_fp32_peak": round(
                 value_per_gpu * gflop_per_unit / 1e3 / PEAK_FP32_TFLOPS, 4)}
 
@@ -485,8 +523,7 @@ def bench_ensemble(args, dev, rank, world, distributed):
         roof["schedule"] = (("timed iterations: the four members on four streams"
                              if ens_streams else "timed iterations: members in order") +
                             "; roofline iterations: eager, members in order")
-        traffic, tsrc = pmc_traffic(roof["kernel"], os.path.join(REPO, "profiles",
-                                                                 "pmc_traffic_ens.json"))
+        traffic, tsrc = pmc_traffic(roof["kernel"], PMC_TRAFFIC_ENS)
         roof["traffic"] = None if traffic is None else round(traffic)
         roof["traffic_unit"] = "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
         roof["traffic_source"] = tsrc or None
