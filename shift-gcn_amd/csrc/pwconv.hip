@@ -86,6 +86,13 @@ __device__ unsigned long long* g_pw_stamps;
 #else
 #define SGCN_PW_STAMP(i) do {} while (0)
 #endif
+// Diagnostic builds only (tools/bench/pwbench -DSGCN_PW_DIAG=n): drop parts of the forward
+// contraction's main loop to see what each costs (results are then wrong): 1 = no A
+// staging after stage 0, 2 = no B staging after stage 0, 3 = neither
+// (profiles/r03_pw/staging_cost.txt).
+#ifndef SGCN_PW_DIAG
+#define SGCN_PW_DIAG 0
+#endif
 
 __device__ __forceinline__ int pmod(int a, int V) {
   int r = a % V;
@@ -263,7 +270,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   auto load_stage = [&](int k0) {
     int cv = cv0;
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
+    for (int i = 0; i < ((SGCN_PW_DIAG & 2) && k0 ? 0 : B_PER); ++i) {
       const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
       if (TSH) {
         // four taps of H around (t + y1, v + x1); a tap outside the plane is masked in
@@ -294,12 +301,13 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
     }
     const unsigned ak0 = AMC ? (unsigned)(k0 * lda * 4) : (unsigned)(k0 * 4);
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) ra[i] = bload(ar, avoff, ak0 + (unsigned)i * astep);
+    for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i)
+      ra[i] = bload(ar, avoff, ak0 + (unsigned)i * astep);
   };
   const int T = p.T;
   auto store_stage = [&](int buf, int k0) {
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
+    for (int i = 0; i < ((SGCN_PW_DIAG & 2) && k0 ? 0 : B_PER); ++i) {
       float val = MASK ? rb[i] * rm[i] : rb[i];
       if (TSH) {
         const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
@@ -322,7 +330,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
       for (int i = 0; i < A_PER; ++i) ra[i] = keep(ra[i], k0 + ak < K);
     }
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
+    for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i) {
       const int m = AMC ? am : am + i * (NT / BK);
       const int k = AMC ? ak + i * (NT / BM) : ak;
       As[buf][k * AP + m] = ra[i];
