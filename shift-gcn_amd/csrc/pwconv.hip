@@ -457,6 +457,8 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
 // ------------------------------------------------------------------------------------
 // dW (split-K over all positions)
 // ------------------------------------------------------------------------------------
+constexpr int kDwBK = 64;   // pw_dw_kernel positions per chunk
+
 struct DwArgs {
   Plane g;            // A operand rows m: G(b, m, n)
   Plane x;            // B operand rows n: X(b, c, n)
@@ -471,7 +473,10 @@ struct DwArgs {
 template <int BM, int BN, int WM, int WN, bool MASK>
 __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
   constexpr int NT = 64 * WM * WN;
-  constexpr int BK = 32;
+  // positions per chunk: a wave's 64 lanes read 64 consecutive positions (256 B) of one
+  // operand row per load instruction (32 lanes x 2 rows, i.e. 128-B row segments, at BK =
+  // 32 read at ~3.7 TB/s on the HBM-bound 64-wide shapes)
+  constexpr int BK = kDwBK;
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
   constexpr int AP = BM + 1, BP = BN + 1;
   constexpr int RSTEP = NT / BK;             // rows per load step
@@ -609,12 +614,12 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
       }
   }
   if (want_bias) {
-    // rows r0 + i*RSTEP are shared by the BK (= 32) lanes with equal tid/BK
+    // rows r0 + i*RSTEP are shared by the BK lanes with equal tid/BK
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       float s = rsum[i];
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      for (int o = BK / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
       const int m = m0 + r0 + i * RSTEP;
       if (kq == 0 && m < p.M) p.bslab[(size_t)split * p.M + m] = s;
     }
@@ -966,7 +971,7 @@ size_t dw3_ws_bytes(int B, int M, int Nc, int T, int V) {
 
 int dw_splits(int M, int Nc, int B, int N, int tiles) {
   // ~512 workgroups (2 per CU at this kernel's register budget); slab <= 16 MiB
-  const int total = B * ((N + 31) / 32);
+  const int total = B * ((N + kDwBK - 1) / kDwBK);
   int S = (512 + tiles - 1) / tiles;
   const long long cap = (16LL << 20) / (4LL * M * Nc);
   if (S > cap) S = (int)cap;
@@ -1120,7 +1125,7 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
     const int tiles = ((M + bm - 1) / bm) * ((Nc + bn - 1) / bn);
     const int N = T * V;
     S = dw_splits(M, Nc, B, N, tiles);
-    const int total = B * ((N + 31) / 32);
+    const int total = B * ((N + kDwBK - 1) / kDwBK);
     a.slab = (float*)ws;
     a.bslab = dbias ? (float*)ws + (size_t)S * M * Nc : nullptr;
     a.chunks_per_split = (total + S - 1) / S;

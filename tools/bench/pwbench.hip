@@ -42,7 +42,7 @@ void dw_variant(const char* name, const Shape& s, DwArgs a, int S, hipStream_t s
                 float* dwref, float* dwout, double fl, double by) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.Nc + BN - 1) / BN);
   const int N = a.T * a.V;
-  const int total = a.B * ((N + 31) / 32);
+  const int total = a.B * ((N + kDwBK - 1) / kDwBK);
   if (S > total) S = total;
   if ((size_t)S * a.M * a.Nc * 4 > ((size_t)256 << 20)) { printf("    S=%d: slab too large, skipped\n", S); return; }
   a.chunks_per_split = (total + S - 1) / S;

@@ -59,11 +59,11 @@ OP_CLASSES = {
 }
 # FETCH_SIZE correction per kernel: x2 for reads whose wave instructions cover whole 128-B
 # lines (calibrated with known-byte kernels: profiles/r02_calib, profiles/r03_fetchcal); the
-# split-K weight-gradient kernels stage 16 / 32 positions per operand row per wave
-# instruction (64-/128-B row segments), for which the counter is NOT calibrated
+# split-K pw_dw3 weight-gradient kernels stage 16 positions per operand row per wave
+# instruction (64-B row segments), for which the counter is NOT calibrated
 # (tools/bench/fetchcal: 0.52x-1.09x of the true bytes raw): reported raw, i.e. a lower
 # bound, with the x2 figure as the upper bound (fetch_bytes_x2_upper).
-UNCALIBRATED = ("pw_dw_kernel", "pw_dw3_kernel")
+UNCALIBRATED = ("pw_dw3_kernel",)
 
 
 def op_traffic(f, w, iters=0):
