@@ -117,6 +117,20 @@ __device__ __forceinline__ void block_sum4(float& a, float& b, float& c, float& 
   d = sd;
 }
 
+// buffer descriptor over [base, base + bytes): 32-bit per-lane voffset + wave-uniform
+// soffset, hardware range check (out-of-range loads return 0, stores are dropped)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, unsigned voff,
+                                       unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+}
+
 // Chan et al. merge of (n, mean, M2) partial statistics, in double.
 struct Moments {
   double n, mean, m2;

@@ -105,20 +105,6 @@ __device__ __forceinline__ float keep(float v, bool ok) {
   return __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
 }
 
-// buffer descriptor over [base, base + bytes): 32-bit per-lane voffset + wave-uniform
-// soffset, hardware range check (out-of-range loads return 0, stores are dropped)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                           0x00020000);
-}
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, unsigned voff,
-                                       unsigned soff) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
-}
-
 // rotation step (d*rsign) mod V in [0, V)
 __device__ __forceinline__ int rot_step(int d, int rsign, int V) { return pmod(d * rsign, V); }
 

@@ -902,6 +902,260 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   }
 }
 
+// Stride-1 backward on a zero-padded LDS plane: the product kernel of every stride-1
+// shift backward (Shift_tcn's shift_in, plain and GBN, and the unit's shift_out, GP).
+// gout is staged with row pitch WP = W + 2 (a zero column each side) between kPadRows zero
+// rows above and below, so for every channel whose shift stays inside the padding
+// (floor(+-x) in {-1, 0}, |floor(+-y)| <= kPadRows - 1 — every channel of a trained
+// Shift-GCN, whose xpos stays near 0 and |ypos| near 1) each tap is an unconditional LDS
+// read at a per-workgroup constant offset from the element: no per-element range checks,
+// clamps or selects (the padding supplies the exact +0 the reference substitutes for an
+// out-of-range tap). A channel whose shift leaves the padding takes the range-checked loop
+// (same values). Global traffic goes through buffer descriptors: the loads
+// need no clamps (past the plane they return 0) and stores past the plane are dropped.
+// Elements are dealt on the joint-aligned stride NTE = (NT / W) * W (a thread's joint is
+// fixed); the sums are the same as tshift_bwd_lds_kernel's, so every output is
+// bit-identical to it (GP / GBN / BNP: see its header).
+constexpr int kPadRows = 4;
+
+__host__ __device__ constexpr int ra_pad_floats(int H, int W) { return (H + 2 * kPadRows) * (W + 2); }
+
+template <int NT, int LPT, bool AFFINE, bool RELU_MASK, bool BNP, bool GP, bool GBN>
+__global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
+    const float* __restrict__ gout, const float* __restrict__ in,
+    const float* __restrict__ xpos, const float* __restrict__ ypos,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
+    float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
+    int H, int W, const float* __restrict__ gdy, const float* __restrict__ gy,
+    const float* __restrict__ gx, const float* __restrict__ gcoef,
+    const float* __restrict__ gz, const float* __restrict__ gzm,
+    const float* __restrict__ gzi, float* __restrict__ gzpart) {
+  static_assert(!GBN || (AFFINE && BNP && !GP), "GBN: shift_in with BNP");
+  extern __shared__ float lds[];   // [(H + 2*kPadRows) * WP] padded gout (GBN: >= 6*NT)
+  __shared__ float red[4 * NT / 64];
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
+  const int c = plane % C;
+  const int n = H * W, WP = W + 2;
+  const int GR = NT / W, NTE = GR * W;
+  const int tid = threadIdx.x;
+  const bool own = tid < NTE;   // the last NT - NTE threads hold no elements
+  const int w = tid % W, h0 = tid / W;
+  // element e of this thread: plane offset e*NTE + tid (bytes vo + e*vstep); a lane that
+  // holds no elements points past every plane (its loads return 0, its stores drop)
+  const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u;
+  const unsigned vstep = (unsigned)NTE * 4u, nbytes = (unsigned)n * 4u;
+  const size_t poff = (size_t)plane * n;
+  float t[LPT], rin_r[LPT];
+  float zr[GBN ? LPT : 1];
+  {   // every global load of the plane in flight together
+    const auto inr = make_rsrc(in + poff, nbytes);
+    if (GP) {
+      const auto dyr = make_rsrc(gdy + poff, nbytes);
+      const auto yr = make_rsrc(gy + poff, nbytes);
+      const auto xr = make_rsrc(gx + poff, nbytes);
+      const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
+      float u1[LPT], u2[LPT];
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) {
+        const unsigned vb = vo + e * vstep;
+        t[e] = bload(dyr, vb, 0);
+        u1[e] = bload(yr, vb, 0);
+        u2[e] = bload(xr, vb, 0);
+        rin_r[e] = bload(inr, vb, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
+    } else {
+      const auto gr = make_rsrc(gout + poff, nbytes);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) {
+        t[e] = bload(gr, vo + e * vstep, 0);
+        rin_r[e] = bload(inr, vo + e * vstep, 0);
+      }
+      if (GBN) {
+        // z is the gcn contraction output BEFORE its shift_out: logical joint w of this
+        // thread sits at (w - c) mod W in its row (a constant in-row offset)
+        const auto zrr = make_rsrc(gz + poff, nbytes);
+        int wz = w - c % W;
+        wz = wz < 0 ? wz + W : wz;
+        const unsigned zo = vo + (unsigned)((wz - w) * 4);
+#pragma unroll
+        for (int e = 0; e < LPT; ++e) zr[e] = bload(zrr, zo + e * vstep, 0);
+      }
+    }
+  }
+  // zero padding: rows [-kPadRows, 0) and [H, H + kPadRows), and the two pad columns
+  const int nprow = 2 * kPadRows * WP;
+  for (int i = tid; i < nprow + 2 * H; i += NT) {
+    int a;
+    if (i < nprow) {
+      const int r = i / WP, col = i - r * WP;
+      a = (r < kPadRows ? r : H + r) * WP + col;
+    } else {
+      const int j = i - nprow;
+      a = ((j >> 1) + kPadRows) * WP + ((j & 1) ? W + 1 : 0);
+    }
+    lds[a] = 0.f;
+  }
+  // element (h, w) of the plane sits at lds[(h + kPadRows) * WP + w + 1]; a lane's elements
+  // past the plane go to the spare float after the padded plane (branch-free stores)
+  const int lbase = (h0 + kPadRows) * WP + w + 1, lstep = GR * WP;
+  const int lspare = ra_pad_floats(H, W);
+#pragma unroll
+  for (int e = 0; e < LPT; ++e)
+    lds[own && e * NTE + tid < n ? lbase + e * lstep : lspare] = t[e];
+  float bmu = 0.f, bis = 0.f;
+  if (BNP) { bmu = bn_mean[c]; bis = bn_invstd[c]; }
+  const float x = xpos[c], y = ypos[c];
+  float a = 1.f, b = 0.f;
+  if (AFFINE) { a = scale[c]; b = shift[c]; }
+  float zm = 0.f, zi = 0.f;
+  if (GBN) { zm = gzm[c * W + w]; zi = gzi[c * W + w]; }
+  __syncthreads();
+
+  // input-gradient taps: gout at (h + r.y1 + {0,1}, w + r.x1 + {0,1}) (.cu:108-150);
+  // position-gradient taps: gout at (h - g.y1 - 1 + {0,1}, w - g.x1 - 1 + {0,1}), i.e.
+  // gout[i - off_k] for the forward taps off_k (exact adjoint, see tshift_bwd_lds_kernel)
+  const Geom r = make_geom(-x, -y);
+  const Geom g = make_geom(x, y);
+  const bool fits = r.y1 >= -kPadRows && r.y1 <= kPadRows - 1 && g.y1 >= -kPadRows &&
+                    g.y1 <= kPadRows - 1 && r.x1 >= -1 && r.x1 <= 0 && g.x1 >= -1 && g.x1 <= 0;
+  const int kq = r.y1 * WP + r.x1, kg = (-g.y1 - 1) * WP - g.x1 - 1;
+  const int nfull = n / NTE;     // elements e < nfull are inside the plane for every lane
+  const int lmax = (H - 1 + kPadRows) * WP + W;   // the last element: past-the-plane bases clamp here
+  const auto gir = make_rsrc(gin + poff, nbytes);
+  float bs0 = 0.f, bs1 = 0.f, ax = 0.f, ay = 0.f;
+  float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // GBN per-joint sums
+  // one element: value, stores and sums from its eight taps (tail: the element may lie
+  // past the plane — its load returned 0, its store drops, its sums are masked here)
+  auto elem = [&](int e, bool tail, float q11, float q21, float q12, float q22, float G11,
+                  float G21, float G12, float G22) {
+    const bool ok = !tail || e * NTE + tid < n;
+    float val = blend(q11, q21, q12, q22, r.dx, r.dy);
+    const float rin = rin_r[e];
+    if (RELU_MASK) val = rin > 0.f ? val : 0.f;
+    if (tail) val = ok ? val : 0.f;
+    bstore(gir, val, vo + e * vstep, 0);   // (an immediate-offset store off one base)
+    if (GBN) {
+      // predicated, not branched (a branch per element keeps every element's registers
+      // live across the blocks): an inactive element adds exact +0 to sums that are
+      // never -0, so the sums are bit-identical to skipping it; rin = 0 past the plane
+      const bool act = rin > 0.f;
+      const float hc = act ? rin - bmu : 0.f, zh = act ? (zr[e] - zm) * zi : 0.f;
+      const float vv = act ? val : 0.f;
+      a6[0] += vv;
+      a6[1] += hc;
+      a6[2] += act ? 1.f : 0.f;
+      a6[3] += vv * zh;
+      a6[4] += hc * zh;
+      a6[5] += zh;
+    }
+    if (BNP) {
+      bs0 += val;
+      bs1 += val * ((rin - bmu) * bis);
+    }
+    const float cx = (1.f - g.dy) * (G21 - G11) + g.dy * (G22 - G12);
+    const float cy = (1.f - g.dx) * (G12 - G11) + g.dx * (G22 - G21);
+    float qa = AFFINE ? rin * a + b : rin;
+    if (tail) qa = ok ? qa : 0.f;
+#ifdef SGCN_EXP_FMA
+    ax = fmaf(qa, cx, ax);
+    ay = fmaf(qa, cy, ay);
+#else
+    ax += qa * cx;
+    ay += qa * cy;
+#endif
+  };
+  if (own && fits) {
+    int l0 = lbase;
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const bool tail = e >= nfull;
+      const int lt = tail ? min(l0, lmax) : l0;
+      const int la = lt + kq, lg = lt + kg;
+      elem(e, tail, lds[la], lds[la + 1], lds[la + WP], lds[la + WP + 1], lds[lg + WP + 1],
+           lds[lg + WP], lds[lg + 1], lds[lg]);
+      // the next element's base is opaque to the compiler: its address arithmetic (and so
+      // its LDS reads) cannot be hoisted into one long-lived register per element
+      l0 += lstep;
+      asm volatile("" : "+v"(l0));
+    }
+  } else if (own) {
+    // range-checked taps (a shift beyond the padding; never in a trained model): a rolled
+    // loop that re-reads its input elements instead of holding the staged registers
+    const auto inr = make_rsrc(in + poff, nbytes);
+    const auto zrr = make_rsrc(GBN ? gz + poff : in + poff, nbytes);
+    int wz = w - c % W;
+    wz = wz < 0 ? wz + W : wz;
+    auto tap = [&](int row, int col) {
+      const bool in_ = (unsigned)row < (unsigned)H && (unsigned)col < (unsigned)W;
+      const int rr = min(max(row, 0), H - 1), cc = min(max(col, 0), W - 1);
+      const float v = lds[(rr + kPadRows) * WP + cc + 1];
+      return in_ ? v : 0.f;
+    };
+#pragma unroll 1
+    for (int e = 0; e < LPT; ++e) {
+      const int h = h0 + e * GR;
+      const bool ok = e * NTE + tid < n;
+      const float rin = bload(inr, vo + e * vstep, 0);
+      const float zv = GBN ? bload(zrr, vo + e * vstep + (unsigned)((wz - w) * 4), 0) : 0.f;
+      const int rq = h + r.y1, cq = w + r.x1, rg = h - g.y1 - 1, cg = w - g.x1 - 1;
+      float val = blend(tap(rq, cq), tap(rq, cq + 1), tap(rq + 1, cq), tap(rq + 1, cq + 1),
+                        r.dx, r.dy);
+      if (RELU_MASK) val = rin > 0.f ? val : 0.f;
+      val = ok ? val : 0.f;
+      bstore(gir, val, vo + e * vstep, 0);
+      if (GBN && rin > 0.f) {
+        const float hc = rin - bmu, zh = (zv - zm) * zi;
+        a6[0] += val;
+        a6[1] += hc;
+        a6[2] += 1.f;
+        a6[3] += val * zh;
+        a6[4] += hc * zh;
+        a6[5] += zh;
+      }
+      if (BNP) {
+        bs0 += val;
+        bs1 += val * ((rin - bmu) * bis);
+      }
+      const float G11 = tap(rg + 1, cg + 1), G21 = tap(rg + 1, cg), G12 = tap(rg, cg + 1),
+                  G22 = tap(rg, cg);
+      const float cx = (1.f - g.dy) * (G21 - G11) + g.dy * (G22 - G12);
+      const float cy = (1.f - g.dx) * (G12 - G11) + g.dx * (G22 - G21);
+      float qa = AFFINE ? rin * a + b : rin;
+      qa = ok ? qa : 0.f;
+      ax += qa * cx;
+      ay += qa * cy;
+    }
+  }
+  if (BNP) {   // both plane reductions behind one barrier pair
+    block_sum4(ax, ay, bs0, bs1, red);
+    if (tid == 0) {
+      pgrad[plane] = make_float2(ax, ay);
+      bn_part[plane] = make_float2(bs0, bs1);
+    }
+  } else {
+    block_sum2(ax, ay, red);
+    if (tid == 0) pgrad[plane] = make_float2(ax, ay);
+  }
+  if (GBN) {
+    // merge the GR row groups of each joint in fixed order (deterministic)
+    __syncthreads();   // every LDS read of gout is done: reuse the LDS (>= 6*NT floats)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) lds[k * NT + tid] = a6[k];
+    __syncthreads();
+    // one thread per (sum k, joint w): GR dependent LDS reads each instead of 6*GR
+    if (tid < 6 * W) {
+      const size_t np = (size_t)gridDim.x * W;
+      const int k = tid / W, wk = tid - k * W;
+      float sum = 0.f;
+      for (int gg = 0; gg < GR; ++gg) sum += lds[k * NT + gg * W + wk];
+      gzpart[k * np + (size_t)plane * W + wk] = sum;
+    }
+  }
+}
+
 // mean over the batch of the per-plane sums (== mean_b then sum_w, sum_h of .cu:501-509
 // up to rounding), then applyShiftConstraint (.cu:370-395) with its float/double
 // promotions: sqrt(dy*dy) in float (correctly rounded), quotients in float, times the
@@ -1068,6 +1322,38 @@ int ra_lpt(int n, int nt, int W) {
 // backward (bnin) keeps 512 threads above 4,096 floats (no difference)
 constexpr int kRaSplit256 = 8192;
 
+// LDS bytes of the padded stride-1 backward (GBN reuses it for 6*NT partial sums)
+size_t ra_lds_bytes(int H, int W, int nt, bool gbn) {
+  const int f = ra_pad_floats(H, W);
+  return (size_t)(gbn ? max(f + 1, 6 * nt) : f + 1) * sizeof(float);   // + the spare float
+}
+constexpr size_t kRaLdsMax = 65536;
+
+// launch tshift_bwd_ra_kernel on nt threads (256 or 512) with LPT = ra_lpt(H*W, nt, W);
+// returns false (nothing launched) when the plane does not fit its LDS or registers
+template <bool AFFINE, bool RELU, bool BNP, bool GP, bool GBN>
+bool launch_ra(int nt, const float* gout, const float* in, const float* xpos,
+               const float* ypos, const float* scale, const float* shift, const float* bmu,
+               const float* bis, float* gin, float2* pg, float2* bp, int B, int C, int H,
+               int W, const float* gdy, const float* gy, const float* gx, const float* gcoef,
+               const float* gz, const float* gzm, const float* gzi, float* gzpart,
+               hipStream_t st) {
+  const int lpt = ra_lpt(H * W, nt, W);
+  const size_t lds = ra_lds_bytes(H, W, nt, GBN);
+  if (lpt == 0 || lds > kRaLdsMax) return false;
+#define SGCN_RA(NT, L)                                                                         \
+  tshift_bwd_ra_kernel<NT, L, AFFINE, RELU, BNP, GP, GBN><<<B * C, NT, lds, st>>>(             \
+      gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, gdy, gy, gx, gcoef,  \
+      gz, gzm, gzi, gzpart)
+  if (nt == 256) {
+    if (lpt == 8) SGCN_RA(256, 8); else if (lpt == 16) SGCN_RA(256, 16); else SGCN_RA(256, 32);
+  } else {
+    if (lpt == 8) SGCN_RA(512, 8); else if (lpt == 16) SGCN_RA(512, 16); else SGCN_RA(512, 32);
+  }
+#undef SGCN_RA
+  return true;
+}
+
 int pick_ept(int n) {
   const int per = (n + kThreads - 1) / kThreads;
   return per <= 8 ? 8 : (per <= 16 ? 16 : 32);
@@ -1210,20 +1496,11 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
   (void)ypos_is_raw;   // stride 1: the +0.5 of shift.py:17-18 never applies
   hipStream_t st = (hipStream_t)stream;
   float2* pg = (float2*)ws;
-  const size_t lds = (size_t)H * W * sizeof(float);
-#define SGCN_BNIN(NT, L)                                                                       \
-  tshift_bwd_lds_kernel<NT, L, false, true, 1, false, true><<<B * C, NT, lds, st>>>(             \
-      nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, C, H, W, H, \
-      0, dy, y, s, coef)
   const int ntb = H * W <= 4096 ? 256 : 512;
-  const int lpb = ra_lpt(H * W, ntb, W);
-  SGCN_REQUIRE(lpb > 0);   // W <= 64 and <= 32 elements per thread (caller falls back)
-  if (ntb == 256) {
-    if (lpb == 8) SGCN_BNIN(256, 8); else if (lpb == 16) SGCN_BNIN(256, 16); else SGCN_BNIN(256, 32);
-  } else {
-    if (lpb == 8) SGCN_BNIN(512, 8); else if (lpb == 16) SGCN_BNIN(512, 16); else SGCN_BNIN(512, 32);
-  }
-#undef SGCN_BNIN
+  const bool ok = launch_ra<false, true, false, true, false>(
+      ntb, nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, B, C,
+      H, W, dy, y, s, coef, nullptr, nullptr, nullptr, nullptr, st);
+  SGCN_REQUIRE(ok);   // W <= 64, <= 32 elements per thread, padded plane <= 64 KiB (ops.ra_fits)
   SGCN_LAUNCH_CHECK();
   if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
@@ -1256,31 +1533,18 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   hipStream_t st = (hipStream_t)stream;
   float2* pg = (float2*)ws;
   float2* bp = (float2*)bn_part;
-#define SGCN_GBN(NT, L)                                                                        \
-  tshift_bwd_lds_kernel<NT, L, true, false, 1, true, false, true>                               \
-      <<<B * C, NT, (size_t)max(H * W, 6 * NT) * sizeof(float), st>>>(                          \
-          gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, C, H, W,   \
-          H, 0, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part)
   // sgcn_tshift_bwd's stride-1 thread counts; elements per thread from the W-aligned
-  // stride (NT / W) * W
+  // stride (NT / W) * W; 512 threads when 256 would need more than 32 per thread
   const int n = H * W;
-  int ntg = n <= kRaSplit256 ? 256 : kBwdThreads;
-  int lpt = ra_lpt(n, ntg, W);
-  if (lpt == 0 && ntg == 256) {   // > 32 elements per thread on 256: take 512 threads
-    ntg = kBwdThreads;
-    lpt = ra_lpt(n, ntg, W);
-  }
-  SGCN_REQUIRE(lpt > 0);   // elements per thread within the largest LPT (ops.ra_fits)
-  if (ntg == 256) {
-    if (lpt == 8) SGCN_GBN(256, 8);
-    else if (lpt == 16) SGCN_GBN(256, 16);
-    else SGCN_GBN(256, 32);
-  } else {
-    if (lpt == 8) SGCN_GBN(kBwdThreads, 8);
-    else if (lpt == 16) SGCN_GBN(kBwdThreads, 16);
-    else SGCN_GBN(kBwdThreads, 32);
-  }
-#undef SGCN_GBN
+#ifdef SGCN_EXP_GBN512
+  const int ntg = kBwdThreads;
+#else
+  const int ntg = n <= kRaSplit256 && ra_lpt(n, 256, W) ? 256 : kBwdThreads;
+#endif
+  const bool ok = launch_ra<true, false, true, false, true>(
+      ntg, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H,
+      W, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part, st);
+  SGCN_REQUIRE(ok);   // within the largest LPT and 64 KiB of LDS (ops.ra_fits)
   SGCN_LAUNCH_CHECK();
   if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
   SGCN_LAUNCH_CHECK();
@@ -1305,25 +1569,27 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   float2* pg = (float2*)ws;
   float2* bp = (float2*)bn_part;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
-  // stride 1: joint-aligned LDS kernels (W <= 64, <= 32 elements per thread); small planes
-  // (T = 150 / 75) on 256 threads, so fewer lanes idle per workgroup
-  const int nt1 = H * W <= kRaSplit256 ? 256 : kBwdThreads;
-  const int lpt1 = stride == 1 && H > 0 && H * W <= kBwdLdsMax ? ra_lpt(H * W, nt1, W) : 0;
-  if (lpt1) {
-#define SGCN_BWD1(L, NTT)                                                                       \
-  launch_bwd_lds<L, 1, NTT>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean,       \
-                            bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st)
-    if (nt1 == 256) {
-      if (lpt1 == 8) SGCN_BWD1(8, 256); else if (lpt1 == 16) SGCN_BWD1(16, 256); else SGCN_BWD1(32, 256);
+  // stride 1: the padded joint-aligned LDS kernel (W <= 64, <= 32 elements per thread,
+  // <= 64 KiB of LDS); small planes (T = 150 / 75) on 256 threads, so fewer lanes idle per
+  // workgroup; anything else takes the global-tap kernel below
+  if (stride == 1 && H > 0) {
+    const int nt1 = H * W <= kRaSplit256 ? 256 : kBwdThreads;
+    bool done;
+#define SGCN_RA1(A, R, P)                                                                       done = launch_ra<A, R, P, false, false>(nt1, gout, in, xpos, ypos, in_scale, in_shift,                                                 bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, nullptr,                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,                                           nullptr, st)
+    if (bp) {
+      if (aff) { if (relu) SGCN_RA1(true, true, true); else SGCN_RA1(true, false, true); }
+      else { if (relu) SGCN_RA1(false, true, true); else SGCN_RA1(false, false, true); }
     } else {
-      if (lpt1 == 8) SGCN_BWD1(8, kBwdThreads); else if (lpt1 == 16) SGCN_BWD1(16, kBwdThreads);
-      else SGCN_BWD1(32, kBwdThreads);
+      if (aff) { if (relu) SGCN_RA1(true, true, false); else SGCN_RA1(true, false, false); }
+      else { if (relu) SGCN_RA1(false, true, false); else SGCN_RA1(false, false, false); }
     }
-#undef SGCN_BWD1
-    SGCN_LAUNCH_CHECK();
-    if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
-    SGCN_LAUNCH_CHECK();
-    return 0;
+#undef SGCN_RA1
+    if (done) {
+      SGCN_LAUNCH_CHECK();
+      if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
   }
   if (stride == 2 && (H + Ho) * W <= kBwdLdsMax && H > 0) {
     const int lpt = pick_lpt((H + Ho) * W, kBwdThreads);
