@@ -324,6 +324,31 @@ constexpr int kFwdLdsMax = 8192;    // floats of the staged input plane (32 KiB)
 constexpr int kFwdLdsMax2 = 16384;  // ... with 512 threads (e.g. MediaPipe T=300: 9,900)
 constexpr int kBwdLdsMax = 16384;   // floats of the staged gout + input planes (64 KiB)
 
+// Zero-padded LDS planes (the stride-1 backward and the forward kernels below): an H x W
+// plane is staged with row pitch WP = W + 2 (a zero column each side) between kPadRows
+// zero rows above and below, element (h, w) at [(h + kPadRows) * WP + w + 1]; a tap of a
+// shift with floor(x) in {-1, 0} and |floor(y)| < kPadRows then needs no range check.
+constexpr int kPadRows = 4;
+
+__host__ __device__ constexpr int ra_pad_floats(int H, int W) { return (H + 2 * kPadRows) * (W + 2); }
+
+// zero the padding of a padded H x W plane (NT threads)
+template <int NT>
+__device__ __forceinline__ void zero_pad(float* lds, int H, int W) {
+  const int WP = W + 2, nprow = 2 * kPadRows * WP;
+  for (int i = (int)threadIdx.x; i < nprow + 2 * H; i += NT) {
+    int a;
+    if (i < nprow) {
+      const int r = i / WP, col = i - r * WP;
+      a = (r < kPadRows ? r : H + r) * WP + col;
+    } else {
+      const int j = i - nprow;
+      a = ((j >> 1) + kPadRows) * WP + ((j & 1) ? W + 1 : 0);
+    }
+    lds[a] = 0.f;
+  }
+}
+
 // copy n floats src -> lds (optionally x*a+b), all loads of a thread issued before any
 // LDS store; n <= LPT * NT
 template <int NT, int LPT, bool AFFINE>
@@ -420,6 +445,101 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
     }
   }
   if (STATS && threadIdx.x == 0) pstats[plane] = make_float2((float)run_mean, (float)run_m2);
+}
+
+// Forward on a zero-padded LDS plane (the product kernel for W <= 64): staged and walked on
+// the joint-aligned element stride NTJ = (NT / W) * W, so a thread's joint is fixed, its
+// staged elements and its outputs sit at a per-thread base plus a uniform step, and, for a
+// channel whose shift stays inside the padding (every channel of a trained model), each of
+// the four taps is an unconditional LDS read (the padding supplies the reference's exact
+// +0 for an out-of-range tap). A channel whose shift leaves the padding takes the same
+// loop with range-checked taps. Global traffic through buffer descriptors (no clamps;
+// stores past the plane drop). Same expressions in the same order as tshift_fwd_kernel:
+// outputs bit-identical. STATS: two-pass {mean, M2} of the whole plane (every output of
+// the plane is in this workgroup's registers).
+template <int NT, int LPT, bool AFFINE, bool STATS>
+__global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
+    const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
+    const float* __restrict__ ypos, const float* __restrict__ scale,
+    const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
+    int Ho, int stride, int add_half) {
+  extern __shared__ float pl[];   // padded Hb x W input plane (affine applied) + 1 spare
+  __shared__ float red[2 * NT / 64];
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
+  const int c = plane % C;
+  const int WP = W + 2, GR = NT / W, NTJ = GR * W;
+  const int tid = threadIdx.x;
+  const bool own = tid < NTJ;
+  const int w = tid % W, h0 = tid / W;
+  const int nb = Hb * W, n = Ho * W;
+  const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
+  float a = 1.f, b = 0.f;
+  if (AFFINE) { a = scale[c]; b = shift[c]; }
+  {
+    const auto ir = make_rsrc(in + (size_t)plane * nb, (unsigned)nb * 4u);
+    float t[LPT];
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) t[e] = bload(ir, vo + e * vstep, 0);
+    zero_pad<NT>(pl, Hb, W);
+    const int lb = (h0 + kPadRows) * WP + w + 1, spare = ra_pad_floats(Hb, W);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e)
+      pl[own && e * NTJ + tid < nb ? lb + e * GR * WP : spare] = AFFINE ? t[e] * a + b : t[e];
+  }
+  const float y = add_half ? ypos[c] + 0.5f : ypos[c];   // shift.py:17-18 (fp32 add)
+  const Geom g = make_geom(xpos[c], y);
+  __syncthreads();
+  const bool fits = g.y1 >= -kPadRows && (Ho - 1) * stride + g.y1 <= Hb + kPadRows - 2 &&
+                    g.x1 >= -1 && g.x1 <= 0;
+  const auto orr = make_rsrc(out + (size_t)plane * n, (unsigned)n * 4u);
+  const int nfull = n / NTJ;   // elements e < nfull are inside the plane for every lane
+  const int nval = own ? (n - tid + NTJ - 1) / NTJ : 0;   // this lane's elements e < nval
+  float v[LPT];
+  if (fits) {
+    // tap (0, 0) of element e: row (h0 + e*GR)*stride + y1, column w + x1; past the plane
+    // (tail elements) the base clamps to the last element's (its value is discarded)
+    const int la0 = (h0 * stride + g.y1 + kPadRows) * WP + w + g.x1 + 1;
+    const int lmax = ((Ho - 1) * stride + g.y1 + kPadRows) * WP + W + g.x1;
+    const int lstep = GR * stride * WP;
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const bool tail = e >= nfull;
+      const int la = tail ? min(la0 + e * lstep, lmax) : la0 + e * lstep;
+      const float val = blend(pl[la], pl[la + 1], pl[la + WP], pl[la + WP + 1], g.dx, g.dy);
+      v[e] = e < nval ? val : 0.f;
+      bstore(orr, val, vo + e * vstep, 0);
+    }
+  } else {
+    const bool c0 = (unsigned)(w + g.x1) < (unsigned)W, c1 = (unsigned)(w + g.x1 + 1) < (unsigned)W;
+    const int cc0 = min(max(w + g.x1, 0), W - 1) + 1, cc1 = min(max(w + g.x1 + 1, 0), W - 1) + 1;
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const int rr = (h0 + e * GR) * stride + g.y1;
+      const bool r0 = (unsigned)rr < (unsigned)Hb, r1 = (unsigned)(rr + 1) < (unsigned)Hb;
+      const int p0 = (min(max(rr, 0), Hb - 1) + kPadRows) * WP;
+      const int p1 = (min(max(rr + 1, 0), Hb - 1) + kPadRows) * WP;
+      const float q11 = (r0 && c0) ? pl[p0 + cc0] : 0.f, q21 = (r0 && c1) ? pl[p0 + cc1] : 0.f;
+      const float q12 = (r1 && c0) ? pl[p1 + cc0] : 0.f, q22 = (r1 && c1) ? pl[p1 + cc1] : 0.f;
+      const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
+      v[e] = e < nval ? val : 0.f;
+      bstore(orr, val, vo + e * vstep, 0);
+    }
+  }
+  if (STATS) {
+    float s1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) s1 += v[e];
+    s1 = block_sum(s1, red);
+    const float mean = s1 / (float)n;
+    float m2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const float d = v[e] - mean;
+      m2 += e < nval ? d * d : 0.f;
+    }
+    m2 = block_sum(m2, red);
+    if (tid == 0) pstats[plane] = make_float2(mean, m2);
+  }
 }
 
 // Inference Shift_gcn tail fused into the following shift_in forward (shift_gcn.py:137-141
@@ -916,9 +1036,6 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
 // Elements are dealt on the joint-aligned stride NTE = (NT / W) * W (a thread's joint is
 // fixed); the sums are the same as tshift_bwd_lds_kernel's, so every output is
 // bit-identical to it (GP / GBN / BNP: see its header).
-constexpr int kPadRows = 4;
-
-__host__ __device__ constexpr int ra_pad_floats(int H, int W) { return (H + 2 * kPadRows) * (W + 2); }
 
 template <int NT, int LPT, bool AFFINE, bool RELU_MASK, bool BNP, bool GP, bool GBN>
 __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
@@ -946,14 +1063,19 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
   const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u;
   const unsigned vstep = (unsigned)NTE * 4u, nbytes = (unsigned)n * 4u;
   const size_t poff = (size_t)plane * n;
+#ifdef SGCN_EXP_NOLOAD
+  const unsigned lbytes = 0u;   // timing diagnostic: loads dropped by the range check
+#else
+  const unsigned lbytes = nbytes;
+#endif
   float t[LPT], rin_r[LPT];
   float zr[GBN ? LPT : 1];
   {   // every global load of the plane in flight together
-    const auto inr = make_rsrc(in + poff, nbytes);
+    const auto inr = make_rsrc(in + poff, lbytes);
     if (GP) {
-      const auto dyr = make_rsrc(gdy + poff, nbytes);
-      const auto yr = make_rsrc(gy + poff, nbytes);
-      const auto xr = make_rsrc(gx + poff, nbytes);
+      const auto dyr = make_rsrc(gdy + poff, lbytes);
+      const auto yr = make_rsrc(gy + poff, lbytes);
+      const auto xr = make_rsrc(gx + poff, lbytes);
       const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
       float u1[LPT], u2[LPT];
 #pragma unroll
@@ -967,7 +1089,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
 #pragma unroll
       for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
     } else {
-      const auto gr = make_rsrc(gout + poff, nbytes);
+      const auto gr = make_rsrc(gout + poff, lbytes);
 #pragma unroll
       for (int e = 0; e < LPT; ++e) {
         t[e] = bload(gr, vo + e * vstep, 0);
@@ -976,28 +1098,20 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
       if (GBN) {
         // z is the gcn contraction output BEFORE its shift_out: logical joint w of this
         // thread sits at (w - c) mod W in its row (a constant in-row offset)
-        const auto zrr = make_rsrc(gz + poff, nbytes);
+        const auto zrr = make_rsrc(gz + poff, lbytes);
         int wz = w - c % W;
         wz = wz < 0 ? wz + W : wz;
+#ifdef SGCN_EXP_ZCONTIG
+        const unsigned zo = vo;   // timing diagnostic: z read unrotated (wrong sums)
+#else
         const unsigned zo = vo + (unsigned)((wz - w) * 4);
+#endif
 #pragma unroll
         for (int e = 0; e < LPT; ++e) zr[e] = bload(zrr, zo + e * vstep, 0);
       }
     }
   }
-  // zero padding: rows [-kPadRows, 0) and [H, H + kPadRows), and the two pad columns
-  const int nprow = 2 * kPadRows * WP;
-  for (int i = tid; i < nprow + 2 * H; i += NT) {
-    int a;
-    if (i < nprow) {
-      const int r = i / WP, col = i - r * WP;
-      a = (r < kPadRows ? r : H + r) * WP + col;
-    } else {
-      const int j = i - nprow;
-      a = ((j >> 1) + kPadRows) * WP + ((j & 1) ? W + 1 : 0);
-    }
-    lds[a] = 0.f;
-  }
+  zero_pad<NT>(lds, H, W);
   // element (h, w) of the plane sits at lds[(h + kPadRows) * WP + w + 1]; a lane's elements
   // past the plane go to the spare float after the padded plane (branch-free stores)
   const int lbase = (h0 + kPadRows) * WP + w + 1, lstep = GR * WP;
@@ -1067,7 +1181,14 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
     ay += qa * cy;
 #endif
   };
+#ifdef SGCN_EXP_NOCOMP
+  if (own) {   // timing diagnostic: stores only
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) bstore(gir, rin_r[e] + zr[GBN ? e : 0] + lds[lbase], vo + e * vstep, 0);
+  } else if (false) {
+#else
   if (own && fits) {
+#endif
     int l0 = lbase;
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
@@ -1231,7 +1352,7 @@ void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const 
 #define SGCN_FWDL(A, S, J)                                                               \
   tshift_fwd_lds_kernel<NT, LPT, LPT, A, S, J><<<grid, block, lds, st>>>(               \
       in, out, xpos, ypos, scale, shift, ps, C, H, W, Ho, stride, add_half)
-  if (W <= 64) {   // joint-aligned element stride (W <= NT)
+  if (false) {   // (the joint-aligned walk: tshift_fwd_pad_kernel, launch_fwd_pad)
     if (affine) {
       if (stats) SGCN_FWDL(true, true, true); else SGCN_FWDL(true, false, true);
     } else {
@@ -1245,6 +1366,33 @@ void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const 
     }
   }
 #undef SGCN_FWDL
+}
+
+// padded joint-aligned forward (W <= 64): LPT elements per thread on the (NT / W) * W
+// stride; false (nothing launched) when the plane needs more than 32 per thread or
+// more than 64 KiB of LDS
+template <int NT>
+bool launch_fwd_pad(bool affine, bool stats, const float* in, float* out, const float* xpos,
+                    const float* ypos, const float* scale, const float* shift, float2* ps,
+                    int B, int C, int H, int W, int Ho, int stride, int add_half,
+                    hipStream_t st) {
+  if (W > 64) return false;
+  const int ntj = (NT / W) * W, per = (H * W + ntj - 1) / ntj;
+  const int lpt = per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+  const size_t lds = (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float);
+  if (lpt == 0 || lds > 65536) return false;
+#define SGCN_FWDP(L, A, S)                                                                   \
+  tshift_fwd_pad_kernel<NT, L, A, S><<<B * C, NT, lds, st>>>(in, out, xpos, ypos, scale, shift, \
+                                                              ps, C, H, W, Ho, stride, add_half)
+#define SGCN_FWDP_AS(L)                                                                      \
+  do {                                                                                       \
+    if (affine) { if (stats) SGCN_FWDP(L, true, true); else SGCN_FWDP(L, true, false); }     \
+    else { if (stats) SGCN_FWDP(L, false, true); else SGCN_FWDP(L, false, false); }          \
+  } while (0)
+  if (lpt == 8) SGCN_FWDP_AS(8); else if (lpt == 16) SGCN_FWDP_AS(16); else SGCN_FWDP_AS(32);
+#undef SGCN_FWDP_AS
+#undef SGCN_FWDP
+  return true;
 }
 
 template <int EPT, int STRIDE>
@@ -1379,6 +1527,14 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
   const bool aff = in_scale != nullptr, stats = plane_stats != nullptr;
   float2* ps = (float2*)plane_stats;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
+  // padded joint-aligned kernel (W <= 64): 256 threads up to kFwdLdsMax floats, else 512
+  if (H * W <= kFwdLdsMax2 &&
+      (H * W <= kFwdLdsMax
+           ? launch_fwd_pad<kThreads>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st)
+           : launch_fwd_pad<512>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st))) {
+    SGCN_LAUNCH_CHECK();
+    return 0;
+  }
   if (H * W <= kFwdLdsMax) {
     switch (pick_lpt(H * W, kThreads)) {
       case 8: launch_fwd_lds<8>(aff, stats, in, out, xpos, ypos, in_scale, in_shift, ps, B, C, H, W, Ho, stride, ah, st); break;

@@ -13,11 +13,11 @@ if [ -n "$TESTS" ]; then
   tail -1 $OUT/tests.log
 fi
 # extra variants: tools/ab/libshiftgcn_hip_<name>.so for each name in $VARIANTS
-for shape in ${PROBE_SHAPES:-"64 300" "128 150" "256 75"}; do
-  for v in base tree $VARIANTS; do
+for shape in ${PROBE_SHAPES:-64:300 128:150 256:75}; do
+  for v in tree $VARIANTS; do
     if [ $v = tree ]; then unset SGCN_LIB_PATH; else export SGCN_LIB_PATH=$ROOT/tools/ab/libshiftgcn_hip_$v.so; fi
-    timeout -k 10 120 python -u tools/bench/gbn_probe.py $shape > $OUT/probe_${v}_${shape// /_}.txt 2>&1 || { cat $OUT/probe_${v}_${shape// /_}.txt; exit 1; }
-    echo "$v $(tail -1 $OUT/probe_${v}_${shape// /_}.txt)" | tee -a $OUT/probe.txt
+    timeout -k 10 120 python -u tools/bench/gbn_probe.py ${shape/:/ } > $OUT/probe_${v}_${shape/:/_}.txt 2>&1 || { cat $OUT/probe_${v}_${shape/:/_}.txt; exit 1; }
+    echo "$v $(tail -1 $OUT/probe_${v}_${shape/:/_}.txt)" | tee -a $OUT/probe.txt
   done
 done
 unset SGCN_LIB_PATH
