@@ -364,10 +364,8 @@ __device__ __forceinline__ void stage_plane(const float* __restrict__ src, float
   }
 }
 
-// JA: output elements dealt on the joint-aligned stride (NT / W) * W (as the stride-1
-// backward kernels), so the column part of the four taps is a per-thread constant and only
-// the rows are range-checked per element; the values are the same expression
-template <int NT, int EPT, int LPT, bool AFFINE, bool STATS, bool JA = false>
+// The W > 64 fallback of tshift_fwd_pad_kernel (every plane of the model takes that one).
+template <int NT, int EPT, int LPT, bool AFFINE, bool STATS>
 __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
     const float* __restrict__ ypos, const float* __restrict__ scale,
@@ -386,29 +384,9 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
   __syncthreads();
   const int n = Ho * W;
   double run_n = 0.0, run_mean = 0.0, run_m2 = 0.0;  // block-uniform (STATS only)
-  const int NTJ = JA ? (NT / W) * W : NT, GR = NT / W;
-  const bool own = !JA || (int)threadIdx.x < NTJ;
-  const int wj = (int)threadIdx.x % W, wc = wj + g.x1;
-  const bool c0 = (unsigned)wc < (unsigned)W, c1 = (unsigned)(wc + 1) < (unsigned)W;
-  const int cc0 = min(max(wc, 0), W - 1), cc1 = min(max(wc + 1, 0), W - 1);
-  for (int base = 0; base < n; base += EPT * NTJ) {
+  for (int base = 0; base < n; base += EPT * NT) {
     float v[EPT];
-    if (JA) {
-      int h = base / W + (int)threadIdx.x / W;
-#pragma unroll
-      for (int e = 0; e < EPT; ++e, h += GR) {
-        const int o = base + e * NTJ + threadIdx.x;
-        const int rr = h * stride + g.y1;
-        const bool r0 = (unsigned)rr < (unsigned)Hb, r1 = (unsigned)(rr + 1) < (unsigned)Hb;
-        const int p0 = min(max(rr, 0), Hb - 1) * W, p1 = min(max(rr + 1, 0), Hb - 1) * W;
-        const float q11 = (r0 && c0) ? pl[p0 + cc0] : 0.f, q21 = (r0 && c1) ? pl[p0 + cc1] : 0.f;
-        const float q12 = (r1 && c0) ? pl[p1 + cc0] : 0.f, q22 = (r1 && c1) ? pl[p1 + cc1] : 0.f;
-        const bool ok = own && o < n;
-        const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
-        v[e] = ok ? val : 0.f;
-        if (ok) dst[o] = val;
-      }
-    } else {
+    {
       Walker pos(base + threadIdx.x, NT, W);
 #pragma unroll
       for (int e = 0; e < EPT; ++e) {
@@ -424,7 +402,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
       }
     }
     if (STATS) {
-      const int cnt = min(n - base, EPT * NTJ);
+      const int cnt = min(n - base, EPT * NT);
       float s = 0.f;
 #pragma unroll
       for (int e = 0; e < EPT; ++e) s += v[e];
@@ -433,9 +411,9 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
       float m2 = 0.f;
 #pragma unroll
       for (int e = 0; e < EPT; ++e) {
-        const int o = base + e * NTJ + threadIdx.x;
+        const int o = base + e * NT + threadIdx.x;
         const float d = v[e] - mean;
-        m2 += (own && o < n) ? d * d : 0.f;
+        m2 += o < n ? d * d : 0.f;
       }
       m2 = block_sum(m2, red);
       const Moments m = merge({run_n, run_mean, run_m2}, {(double)cnt, (double)mean, (double)m2});
@@ -668,118 +646,35 @@ __global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
   }
 }
 
-// GP (stride 1 only): gout is not read; it is the input gradient of the BatchNorm that
-// follows this shift (Shift_tcn.bn2 inside a TCN_GCN_unit, shift_gcn.py:73,161-162),
-// formed while staging: gout = k1*(gy > 0 ? gdy : 0) + k2*gx + k3 (gdy = the unit's output
-// gradient, gy = its output, gx = bn2's input S, k = sgcn_bn_bwd_finalize coefficients),
-// so that gradient tensor is never written.
-//
-// GBN (stride 1, with AFFINE + BNP: Shift_tcn's shift_in inside a TCN_GCN_unit whose
-// Shift_gcn has no down conv): also the backward partials of Shift_gcn.bn, the per-joint
-// BatchNorm1d whose ReLU output H is this shift's input (shift_gcn.py:137-141), without a
-// separate pass over (dA, H, Z). Its input gradient is g = [H > 0] * (k1*dA + k2*H + k3)
-// with k = Shift_tcn.bn's backward coefficients, which need this launch's own batch-wide
-// partials first; so the k-free sums are emitted per (plane, joint) instead, centred on
-// Shift_tcn.bn's mean mu (k2*H + k3 = k2*(H - mu) + (k3 + k2*mu), no cancellation):
-//   {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh} over t where H > 0,
-//   zh = (Z - zmean[c,v]) * zinvstd[c,v]; sgcn_bn_bwd_finalize_gbn combines them.
-template <int NT, int LPT, bool AFFINE, bool RELU_MASK, int STRIDE, bool BNP, bool GP = false,
-          bool GBN = false, bool JA = false>
-__global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
+// Stride-2 backward (the shift_out of l5 / l8), LDS-staged: both planes staged in one
+// pass. JA (W <= 64): both passes walk their grids on the joint-aligned element stride
+// (NT / W) * W: a thread's joint w is fixed, so the column part of every tap is a
+// per-thread constant, and of the two gout rows an input row can reach (h1 / 2 and
+// (h1 + 1) / 2) exactly one exists, so pass (1) reads 2 taps, not 4 (the other two are the
+// exact zeros the general path selects).
+template <int NT, int LPT, bool AFFINE, bool RELU_MASK, bool BNP, bool JA>
+__global__ __launch_bounds__(NT) void tshift_bwd_s2_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
     float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
-    int Hb, int W, int Ho, int add_half, const float* __restrict__ gdy = nullptr,
-    const float* __restrict__ gy = nullptr, const float* __restrict__ gx = nullptr,
-    const float* __restrict__ gcoef = nullptr, const float* __restrict__ gz = nullptr,
-    const float* __restrict__ gzm = nullptr, const float* __restrict__ gzi = nullptr,
-    float* __restrict__ gzpart = nullptr) {
-  static_assert(!GP || STRIDE == 1, "GP is a stride-1 (re-associated) variant");
-  static_assert(!GBN || (STRIDE == 1 && BNP && !GP), "GBN: stride-1 shift_in with BNP");
-  // JA (stride 2): both planes staged as in the general path, but the two passes walk
-  // their grids on the joint-aligned element stride (NT / W) * W like the stride-1 kernels:
-  // a thread's joint w is fixed, so the column part of every tap is a per-thread constant,
-  // and of the two gout rows an input row can reach (h1 / 2 and (h1 + 1) / 2) exactly one
-  // exists, so pass (1) reads 2 taps, not 4 (the other two are the exact zeros the general
-  // path selects)
-  static_assert(!JA || STRIDE == 2, "JA: the stride-2 joint-aligned walk");
-  // STRIDE == 1 ("re-associated"): only gout is staged (half the LDS -> twice the
-  // workgroups per CU); each thread's own input elements are loaded into registers with
-  // the staging loads, and the position-gradient sums are accumulated over INPUT positions
-  // in pass (1) from the same gout neighbourhood:
-  //   sum_o g[o] * dq(o)/dy = sum_i in[i] * sum_k w'_k g[i - off_k]
-  // (exact adjoint identity; only the summation order differs from the reference's
-  // sum over outputs, and the constraint keeps only the sign of the sum, .cu:370-395).
-  constexpr bool RA = STRIDE == 1;
-  extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input (STRIDE 2 only)]
+    int Hb, int W, int Ho, int add_half) {
+  constexpr int STRIDE = 2;
+  extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input]
   __shared__ float red[4 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
   const int nb = Hb * W, nt = Ho * W;
   float* gs = lds;
   float* xs = lds + nt;
-  float rin_r[RA ? LPT : 1];
   float bmu = 0.f, bis = 0.f;
   if (BNP) { bmu = bn_mean[c]; bis = bn_invstd[c]; }
   const float x = xpos[c];
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
-  // RA (stride 1): elements are dealt to the first NTE = (NT / W) * W threads with stride
-  // NTE, so a thread's joint w = threadIdx.x % W is the same for all its elements: the
-  // column part of every tap is a per-thread constant, and (GBN) the per-joint sums
-  // accumulate in registers (the remaining NT - NTE threads hold no elements)
-  const int NTE = RA ? (NT / W) * W : NT;   // RA: joint-aligned element stride (W <= NT)
-  const bool own = !RA || (int)threadIdx.x < NTE;
-  float zr[GBN ? LPT : 1];
-  if (RA) {   // gout -> LDS, own input elements -> registers, all loads in flight together
-    const float* __restrict__ go = gout + (size_t)plane * nt;
-    const float* __restrict__ src = in + (size_t)plane * nb;
-    float t[LPT];
-    if (GBN) {
-      // z is the gcn contraction output BEFORE its shift_out: logical joint w of this
-      // thread sits at (w - c) mod W in its row (constant in-row offset zd)
-      const float* __restrict__ zp = gz + (size_t)plane * nb;
-      const int w0 = (int)threadIdx.x % W;
-      int wz = w0 - c % W;
-      wz = wz < 0 ? wz + W : wz;
-      const int zd = wz - w0;
-#pragma unroll
-      for (int e = 0; e < LPT; ++e) {
-        const int i = min(e * NTE + (int)threadIdx.x, nt - 1);
-        t[e] = go[i];
-        rin_r[e] = src[i];
-        zr[e] = zp[min(max(i + zd, 0), nb - 1)];
-      }
-    } else if (GP) {
-      const size_t po = (size_t)plane * nt;
-      const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
-      float u1[LPT], u2[LPT];
-#pragma unroll
-      for (int e = 0; e < LPT; ++e) {
-        const int i = min(e * NTE + (int)threadIdx.x, nt - 1);
-        t[e] = gdy[po + i];
-        u1[e] = gy[po + i];
-        u2[e] = gx[po + i];
-        rin_r[e] = src[min(e * NTE + (int)threadIdx.x, nb - 1)];
-      }
-#pragma unroll
-      for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
-    } else {
-#pragma unroll
-      for (int e = 0; e < LPT; ++e) {
-        t[e] = go[min(e * NTE + (int)threadIdx.x, nt - 1)];
-        rin_r[e] = src[min(e * NTE + (int)threadIdx.x, nb - 1)];
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < LPT; ++e) {
-      const int i = e * NTE + threadIdx.x;
-      if (own && i < nt) lds[i] = t[e];
-    }
-  } else {  // one staging pass: both planes' loads in flight together (LPT covers nt + nb)
+  {  // one staging pass: both planes' loads in flight together (LPT covers nt + nb)
     const float* __restrict__ go = gout + (size_t)plane * nt;
     const float* __restrict__ src = in + (size_t)plane * nb;
     const int ntot = nt + nb;
@@ -798,93 +693,10 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
   __syncthreads();
   float* __restrict__ gi = gin + (size_t)plane * nb;
 
-  // (1) grad_input over the bottom grid (.cu:108-150 stride 1; .cu:191-254 stride 2)
+  // (1) grad_input over the bottom grid (.cu:191-254: the even-row rule)
   float bs0 = 0.f, bs1 = 0.f;
   float ax = 0.f, ay = 0.f;
-  float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // GBN per-joint sums (see the header)
-  float zm = 0.f, zi = 0.f;
-  if (GBN) {
-    const int w = (int)threadIdx.x % W;
-    zm = gzm[c * W + w];
-    zi = gzi[c * W + w];
-  }
-  if (RA) {
-    const Geom r = make_geom(-x, -y);
-    const Geom g = make_geom(x, y);
-    // the column part of both tap sets is constant per thread (joint-aligned mapping):
-    // clamped column, in-range mask, and the tap-(0,0) offset relative to the element o;
-    // rows are range-checked per element only when a tap row leaves the plane
-    const int w = (int)threadIdx.x % W, h0 = (int)threadIdx.x / W, GR = NTE / W;
-    const int cr = w + r.x1, cq = w - g.x1 - 1;
-    const bool mr0 = (unsigned)cr < (unsigned)W, mr1 = (unsigned)(cr + 1) < (unsigned)W;
-    const bool mq0 = (unsigned)cq < (unsigned)W, mq1 = (unsigned)(cq + 1) < (unsigned)W;
-    const int kr0 = r.y1 * W - w + min(max(cr, 0), W - 1);
-    const int kr1 = r.y1 * W - w + min(max(cr + 1, 0), W - 1);
-    const int kq0 = (-g.y1 - 1) * W - w + min(max(cq, 0), W - 1);
-    const int kq1 = (-g.y1 - 1) * W - w + min(max(cq + 1, 0), W - 1);
-#pragma unroll
-    for (int e = 0; e < LPT; ++e) {
-      const int o = e * NTE + threadIdx.x;
-      const int h = h0 + e * GR;
-      if (own && o < nb) {
-        float q11, q21, q12, q22;
-        const int rr = h + r.y1;
-        if ((unsigned)rr < (unsigned)(Ho - 1)) {   // both tap rows inside the plane
-          const int p0 = o + kr0, p1 = o + kr1;
-          q11 = mr0 ? gs[p0] : 0.f;
-          q21 = mr1 ? gs[p1] : 0.f;
-          q12 = mr0 ? gs[p0 + W] : 0.f;
-          q22 = mr1 ? gs[p1 + W] : 0.f;
-        } else {
-          TapIdx ti;
-          tap_idx(rr, cr, Ho, W, ti);
-          q11 = sel(gs[ti.o00], ti.m00);
-          q21 = sel(gs[ti.o01], ti.m01);
-          q12 = sel(gs[ti.o10], ti.m10);
-          q22 = sel(gs[ti.o11], ti.m11);
-        }
-        float val = blend(q11, q21, q12, q22, r.dx, r.dy);
-        const float rin = rin_r[e];
-        if (RELU_MASK) val = rin > 0.f ? val : 0.f;
-        gi[o] = val;
-        if (GBN && rin > 0.f) {
-          const float hc = rin - bmu, zh = (zr[e] - zm) * zi;
-          a6[0] += val;
-          a6[1] += hc;
-          a6[2] += 1.f;
-          a6[3] += val * zh;
-          a6[4] += hc * zh;
-          a6[5] += zh;
-        }
-        if (BNP) {
-          bs0 += val;
-          bs1 += val * ((rin - bmu) * bis);
-        }
-        // gout at i - off_k for the forward taps off_k = (y1 + a, x1 + b)
-        float G11, G21, G12, G22;
-        const int rq = h - g.y1 - 1;
-        if ((unsigned)rq < (unsigned)(Ho - 1)) {
-          const int p0 = o + kq0, p1 = o + kq1;
-          G22 = mq0 ? gs[p0] : 0.f;
-          G12 = mq1 ? gs[p1] : 0.f;
-          G21 = mq0 ? gs[p0 + W] : 0.f;
-          G11 = mq1 ? gs[p1 + W] : 0.f;
-        } else {
-          TapIdx tj;
-          tap_idx(rq, cq, Ho, W, tj);
-          G11 = sel(gs[tj.o11], tj.m11);
-          G21 = sel(gs[tj.o10], tj.m10);
-          G12 = sel(gs[tj.o01], tj.m01);
-          G22 = sel(gs[tj.o00], tj.m00);
-        }
-        const float cx = (1.f - g.dy) * (G21 - G11) + g.dy * (G22 - G12);
-        const float cy = (1.f - g.dx) * (G12 - G11) + g.dx * (G22 - G21);
-        const float qa = AFFINE ? rin * a + b : rin;
-        ax += qa * cx;
-        ay += qa * cy;
-      }
-    }
-  } else if (JA) {
+  if (JA) {
     const Geom r = make_geom(-x, -y);
     const int NTJ = (NT / W) * W, GR = NT / W;
     if ((int)threadIdx.x < NTJ && nt > 0) {
@@ -918,10 +730,10 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     for (int o = threadIdx.x; o < nb; o += NT) {
       const int h1 = pos.h + r.y1;
       const int w1 = pos.w + r.x1;
+      // h_im % 2 == 0 (C++ remainder), then h_im / 2 (truncation), bounds on the top grid;
+      // exactly one of h1, h1+1 is even
       TapIdx ti;
-      if (STRIDE == 1) {
-        tap_idx(h1, w1, Ho, W, ti);
-      } else {
+      {
         const int h2 = h1 + 1;
         const int hq1 = (h1 % 2 == 0) ? h1 / 2 : -1;
         const int hq2 = (h2 % 2 == 0) ? h2 / 2 : -1;
@@ -974,7 +786,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
         ay += vy * gg;
       }
     }
-  } else if (!RA) {
+  } else {
     const Geom g = make_geom(x, y);
     Walker pos(threadIdx.x, NT, W);
     for (int o = threadIdx.x; o < nt; o += NT) {
@@ -1004,22 +816,6 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
     block_sum2(ax, ay, red);
     if (threadIdx.x == 0) pgrad[plane] = make_float2(ax, ay);
   }
-  if (GBN) {
-    // merge the G = NTE / W row groups of each joint in fixed order (deterministic)
-    __syncthreads();   // every LDS read of gout is done: reuse the LDS (>= 6*NT floats)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) lds[k * NT + threadIdx.x] = a6[k];
-    __syncthreads();
-    // one thread per (sum k, joint w): G dependent LDS reads each instead of 6*G
-    if ((int)threadIdx.x < 6 * W) {
-      const int G = NTE / W;
-      const size_t np = (size_t)gridDim.x * W;
-      const int k = (int)threadIdx.x / W, w = (int)threadIdx.x - k * W;
-      float sum = 0.f;
-      for (int g = 0; g < G; ++g) sum += lds[k * NT + g * W + w];
-      gzpart[k * np + (size_t)plane * W + w] = sum;
-    }
-  }
 }
 
 // Stride-1 backward on a zero-padded LDS plane: the product kernel of every stride-1
@@ -1034,9 +830,30 @@ __global__ __launch_bounds__(NT) void tshift_bwd_lds_kernel(
 // (same values). Global traffic goes through buffer descriptors: the loads
 // need no clamps (past the plane they return 0) and stores past the plane are dropped.
 // Elements are dealt on the joint-aligned stride NTE = (NT / W) * W (a thread's joint is
-// fixed); the sums are the same as tshift_bwd_lds_kernel's, so every output is
-// bit-identical to it (GP / GBN / BNP: see its header).
-
+// fixed). The input gradient is bit-identical to the oracle; the position-gradient sums are
+// accumulated over INPUT positions from the same gout neighbourhood (exact adjoint:
+//   sum_o g[o] * dq(o)/dy = sum_i in[i] * sum_k w'_k g[i - off_k]
+// only the summation order differs from the reference's sum over outputs, and the
+// constraint keeps only the sign of the sum, .cu:370-395).
+// BNP: also the per-plane BatchNorm-backward partials {sum gin, sum gin*xhat},
+// xhat = (in - bn_mean[c]) * bn_invstd[c], of the BatchNorm that produced this shift's
+// input (Shift_tcn.bn before shift_in): its separate reduction pass disappears.
+//
+// GP: gout is not read; it is the input gradient of the BatchNorm that
+// follows this shift (Shift_tcn.bn2 inside a TCN_GCN_unit, shift_gcn.py:73,161-162),
+// formed while staging: gout = k1*(gy > 0 ? gdy : 0) + k2*gx + k3 (gdy = the unit's output
+// gradient, gy = its output, gx = bn2's input S, k = sgcn_bn_bwd_finalize coefficients),
+// so that gradient tensor is never written.
+//
+// GBN (with AFFINE + BNP: Shift_tcn's shift_in inside a TCN_GCN_unit whose
+// Shift_gcn has no down conv): also the backward partials of Shift_gcn.bn, the per-joint
+// BatchNorm1d whose ReLU output H is this shift's input (shift_gcn.py:137-141), without a
+// separate pass over (dA, H, Z). Its input gradient is g = [H > 0] * (k1*dA + k2*H + k3)
+// with k = Shift_tcn.bn's backward coefficients, which need this launch's own batch-wide
+// partials first; so the k-free sums are emitted per (plane, joint) instead, centred on
+// Shift_tcn.bn's mean mu (k2*H + k3 = k2*(H - mu) + (k3 + k2*mu), no cancellation):
+//   {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh} over t where H > 0,
+//   zh = (Z - zmean[c,v]) * zinvstd[c,v]; sgcn_bn_bwd_finalize_gbn combines them.
 template <int NT, int LPT, bool AFFINE, bool RELU_MASK, bool BNP, bool GP, bool GBN>
 __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
@@ -1063,19 +880,14 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
   const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u;
   const unsigned vstep = (unsigned)NTE * 4u, nbytes = (unsigned)n * 4u;
   const size_t poff = (size_t)plane * n;
-#ifdef SGCN_EXP_NOLOAD
-  const unsigned lbytes = 0u;   // timing diagnostic: loads dropped by the range check
-#else
-  const unsigned lbytes = nbytes;
-#endif
   float t[LPT], rin_r[LPT];
   float zr[GBN ? LPT : 1];
   {   // every global load of the plane in flight together
-    const auto inr = make_rsrc(in + poff, lbytes);
+    const auto inr = make_rsrc(in + poff, nbytes);
     if (GP) {
-      const auto dyr = make_rsrc(gdy + poff, lbytes);
-      const auto yr = make_rsrc(gy + poff, lbytes);
-      const auto xr = make_rsrc(gx + poff, lbytes);
+      const auto dyr = make_rsrc(gdy + poff, nbytes);
+      const auto yr = make_rsrc(gy + poff, nbytes);
+      const auto xr = make_rsrc(gx + poff, nbytes);
       const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
       float u1[LPT], u2[LPT];
 #pragma unroll
@@ -1089,7 +901,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
 #pragma unroll
       for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
     } else {
-      const auto gr = make_rsrc(gout + poff, lbytes);
+      const auto gr = make_rsrc(gout + poff, nbytes);
 #pragma unroll
       for (int e = 0; e < LPT; ++e) {
         t[e] = bload(gr, vo + e * vstep, 0);
@@ -1098,14 +910,10 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
       if (GBN) {
         // z is the gcn contraction output BEFORE its shift_out: logical joint w of this
         // thread sits at (w - c) mod W in its row (a constant in-row offset)
-        const auto zrr = make_rsrc(gz + poff, lbytes);
+        const auto zrr = make_rsrc(gz + poff, nbytes);
         int wz = w - c % W;
         wz = wz < 0 ? wz + W : wz;
-#ifdef SGCN_EXP_ZCONTIG
-        const unsigned zo = vo;   // timing diagnostic: z read unrotated (wrong sums)
-#else
         const unsigned zo = vo + (unsigned)((wz - w) * 4);
-#endif
 #pragma unroll
         for (int e = 0; e < LPT; ++e) zr[e] = bload(zrr, zo + e * vstep, 0);
       }
@@ -1130,7 +938,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
 
   // input-gradient taps: gout at (h + r.y1 + {0,1}, w + r.x1 + {0,1}) (.cu:108-150);
   // position-gradient taps: gout at (h - g.y1 - 1 + {0,1}, w - g.x1 - 1 + {0,1}), i.e.
-  // gout[i - off_k] for the forward taps off_k (exact adjoint, see tshift_bwd_lds_kernel)
+  // gout[i - off_k] for the forward taps off_k (the adjoint above)
   const Geom r = make_geom(-x, -y);
   const Geom g = make_geom(x, y);
   const bool fits = r.y1 >= -kPadRows && r.y1 <= kPadRows - 1 && g.y1 >= -kPadRows &&
@@ -1161,34 +969,24 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
       a6[0] += vv;
       a6[1] += hc;
       a6[2] += act ? 1.f : 0.f;
-      a6[3] += vv * zh;
-      a6[4] += hc * zh;
+      a6[3] = fmaf(vv, zh, a6[3]);
+      a6[4] = fmaf(hc, zh, a6[4]);
       a6[5] += zh;
     }
     if (BNP) {
       bs0 += val;
-      bs1 += val * ((rin - bmu) * bis);
+      bs1 = fmaf(val, (rin - bmu) * bis, bs1);
     }
     const float cx = (1.f - g.dy) * (G21 - G11) + g.dy * (G22 - G12);
     const float cy = (1.f - g.dx) * (G12 - G11) + g.dx * (G22 - G21);
     float qa = AFFINE ? rin * a + b : rin;
     if (tail) qa = ok ? qa : 0.f;
-#ifdef SGCN_EXP_FMA
+    // the plane sums (position-gradient products, BatchNorm partials) are not bit-matched
+    // to any reference order (their summation order is this kernel's own): fused
     ax = fmaf(qa, cx, ax);
     ay = fmaf(qa, cy, ay);
-#else
-    ax += qa * cx;
-    ay += qa * cy;
-#endif
   };
-#ifdef SGCN_EXP_NOCOMP
-  if (own) {   // timing diagnostic: stores only
-#pragma unroll
-    for (int e = 0; e < LPT; ++e) bstore(gir, rin_r[e] + zr[GBN ? e : 0] + lds[lbase], vo + e * vstep, 0);
-  } else if (false) {
-#else
   if (own && fits) {
-#endif
     int l0 = lbase;
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
@@ -1349,21 +1147,13 @@ void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const 
                     hipStream_t st) {
   dim3 grid(B * C), block(NT);
   const size_t lds = (size_t)H * W * sizeof(float);
-#define SGCN_FWDL(A, S, J)                                                               \
-  tshift_fwd_lds_kernel<NT, LPT, LPT, A, S, J><<<grid, block, lds, st>>>(               \
+#define SGCN_FWDL(A, S)                                                                  \
+  tshift_fwd_lds_kernel<NT, LPT, LPT, A, S><<<grid, block, lds, st>>>(                    \
       in, out, xpos, ypos, scale, shift, ps, C, H, W, Ho, stride, add_half)
-  if (false) {   // (the joint-aligned walk: tshift_fwd_pad_kernel, launch_fwd_pad)
-    if (affine) {
-      if (stats) SGCN_FWDL(true, true, true); else SGCN_FWDL(true, false, true);
-    } else {
-      if (stats) SGCN_FWDL(false, true, true); else SGCN_FWDL(false, false, true);
-    }
+  if (affine) {
+    if (stats) SGCN_FWDL(true, true); else SGCN_FWDL(true, false);
   } else {
-    if (affine) {
-      if (stats) SGCN_FWDL(true, true, false); else SGCN_FWDL(true, false, false);
-    } else {
-      if (stats) SGCN_FWDL(false, true, false); else SGCN_FWDL(false, false, false);
-    }
+    if (stats) SGCN_FWDL(false, true); else SGCN_FWDL(false, false);
   }
 #undef SGCN_FWDL
 }
@@ -1422,18 +1212,18 @@ void launch_bwd(bool affine, bool relu, const float* gout, const float* in, cons
 
 constexpr int kBwdThreads = 512;
 
-template <int LPT, int STRIDE, int NT = kBwdThreads, bool JA = false>
-void launch_bwd_lds(bool affine, bool relu, const float* gout, const float* in,
-                    const float* xpos, const float* ypos, const float* scale,
-                    const float* shift, const float* bmu, const float* bis, float* gin,
-                    float2* pg, float2* bp, int B, int C, int H, int W, int Ho, int add_half,
-                    hipStream_t st) {
+template <int LPT, bool JA>
+void launch_bwd_s2(bool affine, bool relu, const float* gout, const float* in,
+                   const float* xpos, const float* ypos, const float* scale,
+                   const float* shift, const float* bmu, const float* bis, float* gin,
+                   float2* pg, float2* bp, int B, int C, int H, int W, int Ho, int add_half,
+                   hipStream_t st) {
+  constexpr int NT = kBwdThreads;
   dim3 grid(B * C), block(NT);
-  const size_t lds = (size_t)(STRIDE == 1 ? Ho : H + Ho) * W * sizeof(float);
+  const size_t lds = (size_t)(H + Ho) * W * sizeof(float);
 #define SGCN_BWDL(A, R, P)                                                                  \
-  tshift_bwd_lds_kernel<NT, LPT, A, R, STRIDE, P, false, false, JA>                  \
-      <<<grid, block, lds, st>>>(gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, \
-                                 H, W, Ho, add_half)
+  tshift_bwd_s2_kernel<NT, LPT, A, R, P, JA><<<grid, block, lds, st>>>(                      \
+      gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, Ho, add_half)
   if (bp) {
     if (affine) {
       if (relu) SGCN_BWDL(true, true, true); else SGCN_BWDL(true, false, true);
@@ -1692,11 +1482,7 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   // sgcn_tshift_bwd's stride-1 thread counts; elements per thread from the W-aligned
   // stride (NT / W) * W; 512 threads when 256 would need more than 32 per thread
   const int n = H * W;
-#ifdef SGCN_EXP_GBN512
-  const int ntg = kBwdThreads;
-#else
   const int ntg = n <= kRaSplit256 && ra_lpt(n, 256, W) ? 256 : kBwdThreads;
-#endif
   const bool ok = launch_ra<true, false, true, false, true>(
       ntg, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H,
       W, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part, st);
@@ -1750,8 +1536,8 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   if (stride == 2 && (H + Ho) * W <= kBwdLdsMax && H > 0) {
     const int lpt = pick_lpt((H + Ho) * W, kBwdThreads);
 #define SGCN_BWDL_LPT(L, J)                                                                   \
-  launch_bwd_lds<L, 2, kBwdThreads, J>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift,     \
-                                       bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, Ho, ah, st)
+  launch_bwd_s2<L, J>(aff, relu, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, \
+                      gin, pg, bp, B, C, H, W, Ho, ah, st)
     if (W <= 64) {   // joint-aligned walk (W <= NT)
       if (lpt == 8) SGCN_BWDL_LPT(8, true); else if (lpt == 16) SGCN_BWDL_LPT(16, true);
       else SGCN_BWDL_LPT(32, true);

@@ -298,6 +298,10 @@ def ra_fits(n, V):
     every plane this accepts."""
     if V > 64 or n > GBN_MAX_PLANE:
         return False
+    # the padded LDS plane (tshift.hip kPadRows zero rows each side, a zero column each
+    # side, one spare float) within 64 KiB
+    if (n // V + 2 * 4) * (V + 2) + 1 > 16384:
+        return False
     nt = 256 if n <= 4096 else 512
     return -(-n // ((nt // V) * V)) <= 32
 

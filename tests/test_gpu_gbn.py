@@ -20,17 +20,22 @@ DEV = "cuda"
 # the last two: planes of 8,100 / 7,920 floats need > 32 elements per thread on 256
 # threads, so the launcher takes 512 (these raised EINVAL before)
 CASES = [(4, 64, 30, 25), (2, 128, 17, 25), (3, 32, 9, 33), (2, 16, 300, 25),
-         (2, 16, 324, 25), (2, 16, 240, 33)]
+         (2, 16, 324, 25), (2, 16, 240, 33),
+         # shifts past the kernel's zero padding (|floor(y)| >= 4, |x| >= 1): the
+         # range-checked loop of tshift_bwd_ra_kernel
+         (2, 16, 40, 25, "wide")]
 
 
-def _setup(B, C, T, V, seed):
+def _setup(B, C, T, V, seed, wide=False):
     from shiftgcn import ops
     g = torch.Generator().manual_seed(seed)
     Z = (torch.randn(B, C, T, V, generator=g) * 2 + 0.5).to(DEV)
     H = torch.relu(torch.randn(B, C, T, V, generator=g) + 0.3).to(DEV)
     dAs = torch.randn(B, C, T, V, generator=g).to(DEV)
     xpos = ((torch.rand(C, generator=g) - 0.5) * 2e-8).to(DEV)
-    ypos = ((torch.rand(C, generator=g) - 0.5) * 4).to(DEV)
+    ypos = ((torch.rand(C, generator=g) - 0.5) * (24 if wide else 4)).to(DEV)
+    if wide:
+        xpos[:4] = torch.tensor([1.5, -2.25, 0.75, -0.5])
     bn_t, bn_g = nn.BatchNorm2d(C).to(DEV), nn.BatchNorm1d(C * V).to(DEV)
     with torch.no_grad():
         bn_t.weight.copy_(torch.rand(C, generator=g) + 0.5)
@@ -51,8 +56,9 @@ def _rel(a, b):
 @pytest.mark.parametrize("case", CASES, ids=["x".join(map(str, c)) for c in CASES])
 def test_gbn_matches_two_pass(case):
     from shiftgcn import ops
-    B, C, T, V = case
-    Z, H, dAs, xpos, ypos, bn_t, bn_g, ast, zst = _setup(B, C, T, V, sum(case))
+    B, C, T, V = case[:4]
+    Z, H, dAs, xpos, ypos, bn_t, bn_g, ast, zst = _setup(B, C, T, V, sum(case[:4]),
+                                                         wide=len(case) > 4)
     dA1, gx1, gy1, part1 = ops.tshift_bwd(dAs, H, xpos, ypos, 1, scale=ast.scale,
                                           shift=ast.shift, bn_stats=ast)
     dA2, gx2, gy2, part2, z6 = ops.tshift_bwd_gbn(dAs, H, xpos, ypos, ast, Z, zst)
