@@ -1014,6 +1014,12 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   a.a_bytes = (unsigned)((long long)M * K * 4);
   a.mask_bytes = mask ? (unsigned)(V * K * 4) : 0u;
   a.relu = rl ? 1 : 0;
+#ifdef SGCN_DIAG_F2_BOUND
+  // timing diagnostic only (tools/ab_variant.sh; results are wrong): the stride-2 residual
+  // conv's read of the unit input is dropped by the range check, i.e. the most any fusion
+  // sharing that read with the `down` conv (verdict r02, row f2) could save
+  if (x_tstride == 2 && !ac) a.x_bytes = 0;
+#endif
   if (M <= 64) launch_pwg<64, 256, 2, 4>(a, ac, st);
   else if (M <= 128) launch_pwg<128, 256, 2, 4>(a, ac, st);
   else launch_pwg<256, 128, 4, 2>(a, ac, st);

@@ -433,14 +433,33 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
 // +0 for an out-of-range tap). A channel whose shift leaves the padding takes the same
 // loop with range-checked taps. Global traffic through buffer descriptors (no clamps;
 // stores past the plane drop). Same expressions in the same order as tshift_fwd_kernel:
-// outputs bit-identical. STATS: two-pass {mean, M2} of the whole plane (every output of
-// the plane is in this workgroup's registers).
-template <int NT, int LPT, bool AFFINE, bool STATS>
+// outputs bit-identical.
+//   MODE 0: the shift (sgcn_tshift_fwd), optional affine taps; STATS: two-pass
+//           {mean, M2} of the whole plane (every output of the plane is in this
+//           workgroup's registers).
+//   MODE 1: the inference Shift_gcn tail fused into the following shift_in forward
+//           (shift_gcn.py:137-141 then :67-68, BatchNorms in eval mode): the staged input
+//           element is a * relu(z*zs[c*W + w] + zt[c*W + w] + res) + b, z the contraction
+//           output (natural layout), res = r (RES 1, identity down) or r*rs[c] + rt[c]
+//           (RES 2, down conv + eval BN), a/b = Shift_tcn.bn (eval); H is never written.
+//   MODE 2: the inference unit tail fused into the shift_out forward (shift_gcn.py:72-73 +
+//           161-162, eval): out = relu(S*ps[c] + pt[c] + res), S the shifted value, res = 0 /
+//           r / r*rs[c] + rt[c] read at the output address; GOUT: also the next Shift_gcn's
+//           gathered, masked input og[c,t,(v - c) mod V] = out[c,t,v] * gm[((v - c) mod V)*C
+//           + c]. S is never written.
+// A thread's joint is fixed, so the per-joint tables (zs/zt, the gather's mask and target
+// joint) are per-thread constants.
+template <int NT, int LPT, int MODE, bool AFFINE, bool STATS, int RES = 0, bool GOUT = false>
 __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ xpos,
     const float* __restrict__ ypos, const float* __restrict__ scale,
     const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
-    int Ho, int stride, int add_half) {
+    int Ho, int stride, int add_half, const float* __restrict__ zs = nullptr,
+    const float* __restrict__ zt = nullptr, const float* __restrict__ r = nullptr,
+    const float* __restrict__ rs = nullptr, const float* __restrict__ rt = nullptr,
+    const float* __restrict__ gm = nullptr, float* __restrict__ og = nullptr) {
+  static_assert(MODE != 1 || (AFFINE && RES >= 1 && !STATS), "pre: affine taps of relu(...)");
+  static_assert(MODE != 2 || (!AFFINE && !STATS), "tail: plain taps");
   extern __shared__ float pl[];   // padded Hb x W input plane (affine applied) + 1 spare
   __shared__ float red[2 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
@@ -453,26 +472,73 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
   const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
+  float q1 = 1.f, q2 = 0.f;   // residual BatchNorm (RES 2)
+  if (RES == 2) { q1 = rs[c]; q2 = rt[c]; }
   {
     const auto ir = make_rsrc(in + (size_t)plane * nb, (unsigned)nb * 4u);
-    float t[LPT];
+    float t[LPT], u[MODE == 1 ? LPT : 1];
 #pragma unroll
     for (int e = 0; e < LPT; ++e) t[e] = bload(ir, vo + e * vstep, 0);
+    if (MODE == 1) {
+      const auto rr = make_rsrc(r + (size_t)plane * nb, (unsigned)nb * 4u);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) u[e] = bload(rr, vo + e * vstep, 0);
+    }
+    float zsw = 0.f, ztw = 0.f;
+    if (MODE == 1) { zsw = zs[c * W + w]; ztw = zt[c * W + w]; }
     zero_pad<NT>(pl, Hb, W);
     const int lb = (h0 + kPadRows) * WP + w + 1, spare = ra_pad_floats(Hb, W);
 #pragma unroll
-    for (int e = 0; e < LPT; ++e)
-      pl[own && e * NTJ + tid < nb ? lb + e * GR * WP : spare] = AFFINE ? t[e] * a + b : t[e];
+    for (int e = 0; e < LPT; ++e) {
+      float val = t[e];
+      if (MODE == 1) {
+        float h = t[e] * zsw + ztw;
+        h += RES == 2 ? u[e] * q1 + q2 : u[e];
+        val = fmaxf(h, 0.f);
+      }
+      pl[own && e * NTJ + tid < nb ? lb + e * GR * WP : spare] = AFFINE ? val * a + b : val;
+    }
   }
   const float y = add_half ? ypos[c] + 0.5f : ypos[c];   // shift.py:17-18 (fp32 add)
   const Geom g = make_geom(xpos[c], y);
+  const size_t ooff = (size_t)plane * n;
+  float rv[MODE == 2 && RES ? LPT : 1];
+  if (MODE == 2 && RES) {   // the residual at the output addresses, in flight over the barrier
+    const auto rr = make_rsrc(r + ooff, (unsigned)n * 4u);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) rv[e] = bload(rr, vo + e * vstep, 0);
+  }
+  float sc = 1.f, sh = 0.f, gmu = 0.f;
+  int du = 0;
+  if (MODE == 2) {
+    sc = scale[c];
+    sh = shift[c];
+    if (GOUT) {
+      int uu = w - c % W;
+      uu = uu < 0 ? uu + W : uu;
+      du = uu - w;
+      gmu = gm[uu * C + c];
+    }
+  }
   __syncthreads();
   const bool fits = g.y1 >= -kPadRows && (Ho - 1) * stride + g.y1 <= Hb + kPadRows - 2 &&
                     g.x1 >= -1 && g.x1 <= 0;
-  const auto orr = make_rsrc(out + (size_t)plane * n, (unsigned)n * 4u);
+  const auto orr = make_rsrc(out + ooff, (unsigned)n * 4u);
+  const auto ogr = make_rsrc(GOUT ? og + ooff : out + ooff, GOUT ? (unsigned)n * 4u : 0u);
   const int nfull = n / NTJ;   // elements e < nfull are inside the plane for every lane
   const int nval = own ? (n - tid + NTJ - 1) / NTJ : 0;   // this lane's elements e < nval
-  float v[LPT];
+  float v[STATS ? LPT : 1];
+  auto emit = [&](int e, float val) {
+    if (MODE == 2) {
+      float aa = val * sc + sh;
+      if (RES == 1) aa += rv[e];
+      if (RES == 2) aa += rv[e] * q1 + q2;
+      val = fmaxf(aa, 0.f);
+    }
+    if (STATS) v[e] = e < nval ? val : 0.f;
+    bstore(orr, val, vo + e * vstep, 0);
+    if (GOUT) bstore(ogr, val * gmu, vo + e * vstep + (unsigned)(du * 4), 0);
+  };
   if (fits) {
     // tap (0, 0) of element e: row (h0 + e*GR)*stride + y1, column w + x1; past the plane
     // (tail elements) the base clamps to the last element's (its value is discarded)
@@ -483,9 +549,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     for (int e = 0; e < LPT; ++e) {
       const bool tail = e >= nfull;
       const int la = tail ? min(la0 + e * lstep, lmax) : la0 + e * lstep;
-      const float val = blend(pl[la], pl[la + 1], pl[la + WP], pl[la + WP + 1], g.dx, g.dy);
-      v[e] = e < nval ? val : 0.f;
-      bstore(orr, val, vo + e * vstep, 0);
+      emit(e, blend(pl[la], pl[la + 1], pl[la + WP], pl[la + WP + 1], g.dx, g.dy));
     }
   } else {
     const bool c0 = (unsigned)(w + g.x1) < (unsigned)W, c1 = (unsigned)(w + g.x1 + 1) < (unsigned)W;
@@ -498,9 +562,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
       const int p1 = (min(max(rr + 1, 0), Hb - 1) + kPadRows) * WP;
       const float q11 = (r0 && c0) ? pl[p0 + cc0] : 0.f, q21 = (r0 && c1) ? pl[p0 + cc1] : 0.f;
       const float q12 = (r1 && c0) ? pl[p1 + cc0] : 0.f, q22 = (r1 && c1) ? pl[p1 + cc1] : 0.f;
-      const float val = blend(q11, q21, q12, q22, g.dx, g.dy);
-      v[e] = e < nval ? val : 0.f;
-      bstore(orr, val, vo + e * vstep, 0);
+      emit(e, blend(q11, q21, q12, q22, g.dx, g.dy));
     }
   }
   if (STATS) {
@@ -1158,6 +1220,15 @@ void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const 
 #undef SGCN_FWDL
 }
 
+// elements per thread of the padded joint-aligned forward kernels (W <= 64) on NT threads;
+// 0 when the plane needs more than 32 per thread or more than 64 KiB of LDS
+int pad_fwd_lpt(int H, int W, int nt) {
+  if (W > 64) return 0;
+  const int ntj = (nt / W) * W, per = (H * W + ntj - 1) / ntj;
+  const int lpt = per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+  return (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float) > 65536 ? 0 : lpt;
+}
+
 // padded joint-aligned forward (W <= 64): LPT elements per thread on the (NT / W) * W
 // stride; false (nothing launched) when the plane needs more than 32 per thread or
 // more than 64 KiB of LDS
@@ -1166,13 +1237,11 @@ bool launch_fwd_pad(bool affine, bool stats, const float* in, float* out, const 
                     const float* ypos, const float* scale, const float* shift, float2* ps,
                     int B, int C, int H, int W, int Ho, int stride, int add_half,
                     hipStream_t st) {
-  if (W > 64) return false;
-  const int ntj = (NT / W) * W, per = (H * W + ntj - 1) / ntj;
-  const int lpt = per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+  const int lpt = pad_fwd_lpt(H, W, NT);
   const size_t lds = (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float);
-  if (lpt == 0 || lds > 65536) return false;
+  if (lpt == 0) return false;
 #define SGCN_FWDP(L, A, S)                                                                   \
-  tshift_fwd_pad_kernel<NT, L, A, S><<<B * C, NT, lds, st>>>(in, out, xpos, ypos, scale, shift, \
+  tshift_fwd_pad_kernel<NT, L, 0, A, S><<<B * C, NT, lds, st>>>(in, out, xpos, ypos, scale, shift, \
                                                               ps, C, H, W, Ho, stride, add_half)
 #define SGCN_FWDP_AS(L)                                                                      \
   do {                                                                                       \
@@ -1363,6 +1432,28 @@ int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const flo
   SGCN_REQUIRE((long long)B * C < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
+  {   // padded joint-aligned kernel (W <= 64)
+    const int nt = H * W <= kFwdLdsMax ? kThreads : 512;
+    const int lpt = pad_fwd_lpt(H, W, nt);
+    if (lpt) {
+      const size_t plds = (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float);
+#define SGCN_PREP(NT, L, R)                                                                    \
+  tshift_fwd_pad_kernel<NT, L, 1, true, false, R><<<B * C, NT, plds, st>>>(                    \
+      z, out, xpos, ypos, in_scale, in_shift, nullptr, C, H, W, Ho, stride, ah, pre_scale,      \
+      pre_shift, r, r_scale, r_shift)
+#define SGCN_PREP_R(NT, L) \
+  do { if (r_scale) SGCN_PREP(NT, L, 2); else SGCN_PREP(NT, L, 1); } while (0)
+      if (nt == kThreads) {
+        if (lpt == 8) SGCN_PREP_R(kThreads, 8); else if (lpt == 16) SGCN_PREP_R(kThreads, 16); else SGCN_PREP_R(kThreads, 32);
+      } else {
+        if (lpt == 8) SGCN_PREP_R(512, 8); else if (lpt == 16) SGCN_PREP_R(512, 16); else SGCN_PREP_R(512, 32);
+      }
+#undef SGCN_PREP_R
+#undef SGCN_PREP
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   const size_t lds = (size_t)H * W * sizeof(float);
 #define SGCN_PRE(NT, L, R)                                                                     \
   tshift_fwd_pre_kernel<NT, L, R><<<B * C, NT, lds, st>>>(z, out, xpos, ypos, pre_scale,       \
@@ -1403,6 +1494,32 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
   const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
   const int res = r == nullptr ? 0 : (r_scale ? 2 : 1);
   const bool go = out_gathered != nullptr;
+  {   // padded joint-aligned kernel (W <= 64)
+    const int nt = H * W <= kFwdLdsMax ? kThreads : 512;
+    const int lpt = pad_fwd_lpt(H, W, nt);
+    if (lpt) {
+      const size_t plds = (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float);
+#define SGCN_TAILP(NT, L, R, G)                                                                \
+  tshift_fwd_pad_kernel<NT, L, 2, false, false, R, G><<<B * C, NT, plds, st>>>(                \
+      in, out, xpos, ypos, post_scale, post_shift, nullptr, C, H, W, Ho, stride, ah, nullptr,  \
+      nullptr, r, r_scale, r_shift, gather_m, out_gathered)
+#define SGCN_TAILP_RG(NT, L)                                                                   \
+  do {                                                                                         \
+    if (res == 0) { if (go) SGCN_TAILP(NT, L, 0, true); else SGCN_TAILP(NT, L, 0, false); }    \
+    else if (res == 1) { if (go) SGCN_TAILP(NT, L, 1, true); else SGCN_TAILP(NT, L, 1, false); } \
+    else { if (go) SGCN_TAILP(NT, L, 2, true); else SGCN_TAILP(NT, L, 2, false); }             \
+  } while (0)
+      if (nt == kThreads) {
+        if (lpt == 8) SGCN_TAILP_RG(kThreads, 8); else if (lpt == 16) SGCN_TAILP_RG(kThreads, 16); else SGCN_TAILP_RG(kThreads, 32);
+      } else {
+        if (lpt == 8) SGCN_TAILP_RG(512, 8); else if (lpt == 16) SGCN_TAILP_RG(512, 16); else SGCN_TAILP_RG(512, 32);
+      }
+#undef SGCN_TAILP_RG
+#undef SGCN_TAILP
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   const size_t lds = (size_t)H * W * sizeof(float);
 #define SGCN_TAIL(NT, L, R, G)                                                                \
   tshift_fwd_tail_kernel<NT, L, R, G><<<B * C, NT, lds, st>>>(                                \
