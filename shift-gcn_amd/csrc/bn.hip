@@ -302,6 +302,84 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
   }
 }
 
+// Plane-resident form of bn_apply_kernel (the product kernel for V <= 64 and planes of
+// <= 32 elements per thread): one workgroup per (n·m, c) plane holds the whole plane in
+// registers, dealt on the joint-aligned stride NTJ = (NT / V) * V, so a thread's (logical)
+// joint w is fixed: the per-joint coefficients, the ZU source offset (the pre-shift_out
+// element of logical joint w sits at (w - c) mod V in its row) and the gather target /
+// mask of OUTX = 2 are per-thread constants, and every load of the plane is in flight at
+// once (buffer descriptors: no clamps, stores past the plane drop). Same expressions as
+// bn_apply_kernel, so y / yg are bit-identical; OUTX = 1 takes the plane's {mean, M2} by
+// two passes over the registers.
+template <int NT, int LPT, bool PER_JOINT, int RES, bool RELU, int OUTX, bool ZU>
+__global__ __launch_bounds__(NT) void bn_apply_ja_kernel(
+    const float* __restrict__ x, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ r,
+    const float* __restrict__ rscale, const float* __restrict__ rshift,
+    float* __restrict__ y, float2* __restrict__ ystats, const float* __restrict__ gm,
+    float* __restrict__ yg, int C, int T, int V) {
+  constexpr bool OUT_STATS = OUTX == 1, OUT_G = OUTX == 2;
+  __shared__ float red[2 * NT / 64];
+  const int plane = blockIdx.x, c = plane % C, rc = c % V;
+  const int GR = NT / V, NTJ = GR * V, tid = threadIdx.x;
+  const bool own = tid < NTJ;
+  const int w = tid % V;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
+  const unsigned pb = (unsigned)P * 4u;
+  // ZU: the source element of logical joint w; OUT_G: its gather target (both in-row)
+  int wz = w - rc;
+  wz = wz < 0 ? wz + V : wz;
+  const unsigned xo = vo + (unsigned)((ZU ? wz - w : 0) * 4);
+  const unsigned go = vo + (unsigned)((wz - w) * 4);
+  float xv[LPT], rv[RES ? LPT : 1];
+  {
+    const auto xr = make_rsrc(x + off, pb);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) xv[e] = bload(xr, xo + e * vstep, 0);
+    if (RES) {
+      const auto rr = make_rsrc(r + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) rv[e] = bload(rr, vo + e * vstep, 0);
+    }
+  }
+  const float sc = PER_JOINT ? scale[c * V + w] : scale[c];
+  const float sh = PER_JOINT ? shift[c * V + w] : shift[c];
+  float rsc = 1.f, rsh = 0.f;
+  if (RES == 2) { rsc = rscale[c]; rsh = rshift[c]; }
+  const float gmu = OUT_G ? gm[wz * C + c] : 0.f;
+  const auto yr = make_rsrc(y + off, pb);
+  const auto ygr = make_rsrc(OUT_G ? yg + off : y + off, OUT_G ? pb : 0u);
+  const int nval = own ? (P - tid + NTJ - 1) / NTJ : 0;   // this lane's elements e < nval
+  float s1 = 0.f;
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    float a = xv[e] * sc + sh;
+    if (RES == 1) a += rv[e];
+    if (RES == 2) a += rv[e] * rsc + rsh;
+    if (RELU) a = fmaxf(a, 0.f);
+    bstore(yr, a, vo + e * vstep, 0);
+    if (OUT_G) bstore(ygr, a * gmu, go + e * vstep, 0);
+    if (OUT_STATS) {
+      xv[e] = e < nval ? a : 0.f;   // keep y for the second pass
+      s1 += xv[e];
+    }
+  }
+  if (OUT_STATS) {
+    s1 = block_sum(s1, red);
+    const float mean = s1 / (float)P;
+    float m2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      const float d = xv[e] - mean;
+      m2 += e < nval ? d * d : 0.f;
+    }
+    m2 = block_sum(m2, red);
+    if (tid == 0) ystats[plane] = make_float2(mean, m2);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // backward: reductions of g = dy*(y>0) and g*xhat per feature
 // ------------------------------------------------------------------------------------
@@ -554,6 +632,155 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   }
 }
 
+// Plane-resident form of bn_bwd_apply_kernel (V <= 64, <= 32 elements per thread): the
+// whole plane in registers on the joint-aligned stride, all loads in flight at once; a
+// thread's joint is fixed, so the per-joint coefficients and the PJM 3 gathered index
+// (element (c, t, v) at (c, t, (v - c) mod V)) are per-thread constants. Same expressions
+// as bn_bwd_apply_kernel: outputs bit-identical.
+template <int NT, int LPT, int PJM, bool RELU, int RES, bool DYT>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_ja_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
+    const float* __restrict__ coef, int F, const float* __restrict__ r,
+    const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
+    float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V) {
+  static_assert(PJM == 0 || PJM == 3, "per-channel, or per-joint gathered (ZU)");
+  constexpr bool PER_JOINT = PJM == 3;
+  const int plane = blockIdx.x, c = plane % C, rc = c % V;
+  const int GR = NT / V, NTJ = GR * V, tid = threadIdx.x;
+  const bool own = tid < NTJ;
+  const int w = tid % V;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
+  const unsigned pb = (unsigned)P * 4u;
+  int wz = w - rc;
+  wz = wz < 0 ? wz + V : wz;
+  const unsigned go = vo + (unsigned)((PER_JOINT ? wz - w : 0) * 4);   // dx (and x) index
+  float gv[LPT], yv[RELU ? LPT : 1], xv[LPT], rv[RES == 2 ? LPT : 1];
+  {
+    const auto dyr = make_rsrc(dy + off, pb);
+    const auto xr = make_rsrc(x + off, pb);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      gv[e] = bload(dyr, vo + e * vstep, 0);
+      xv[e] = bload(xr, go + e * vstep, 0);
+    }
+    if (RELU) {
+      const auto yr = make_rsrc(y + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) yv[e] = bload(yr, vo + e * vstep, 0);
+    }
+    if (RES == 2) {
+      const auto rr = make_rsrc(r + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) rv[e] = bload(rr, vo + e * vstep, 0);
+    }
+  }
+  const int f = PER_JOINT ? c * V + w : c;
+  const float k1 = coef[f], k2 = coef[F + f], k3 = coef[2 * F + f];
+  float d1 = 1.f, d2 = 0.f, d3 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+  if (DYT) { d1 = dyc[c]; d2 = dyc[C + c]; d3 = dyc[2 * C + c]; }
+  if (RES == 2) { q1 = rcoef[c]; q2 = rcoef[RF + c]; q3 = rcoef[2 * RF + c]; }
+  const auto dxr = make_rsrc(dx + off, pb);
+  const auto drr = make_rsrc(RES ? dr + off : dx + off, RES ? pb : 0u);
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    float g = gv[e];
+    if (DYT) g = d1 * g + d2 * yv[e] + d3;
+    if (RELU) g = yv[e] > 0.f ? g : 0.f;
+    bstore(dxr, k1 * g + k2 * xv[e] + k3, go + e * vstep, 0);
+    if (RES == 1) bstore(drr, g, vo + e * vstep, 0);
+    if (RES == 2) bstore(drr, q1 * g + q2 * rv[e] + q3, vo + e * vstep, 0);
+  }
+}
+
+// Plane-resident form of gcn_dx_finish_kernel (V <= 64, <= 32 elements per thread): the
+// same one-pass assignment (a thread owns destination joint v' and so source joint
+// u = (v' - c) mod V: one mask value, one dmask accumulator), with the whole plane's loads
+// in flight at once. dx is bit-identical; the plane sums only change order.
+template <int NT, int LPT, bool ADD1, bool ADD2, bool PART, bool A2M>
+__global__ __launch_bounds__(NT) void gcn_dx_finish_ja_kernel(
+    const float* __restrict__ dxt, const float* __restrict__ x0, const float* __restrict__ m,
+    const float* __restrict__ add1, const float* __restrict__ add2, float* __restrict__ dx,
+    float* __restrict__ dmask_part, const float* __restrict__ ps,
+    const float* __restrict__ pmean, const float* __restrict__ pinvstd,
+    float2* __restrict__ bn_part, int C, int T, int V, const float* __restrict__ add2m) {
+  __shared__ float s0[NT];
+  __shared__ float red[2 * NT / 64];
+  const int plane = blockIdx.x, c = plane % C, rc = c % V;
+  const int GR = NT / V, NTJ = GR * V, tid = threadIdx.x;
+  const bool own = tid < NTJ;
+  const int vd = tid % V;
+  int us = vd - rc;
+  us = us < 0 ? us + V : us;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
+  const unsigned pb = (unsigned)P * 4u;
+  const unsigned uo = vo + (unsigned)((us - vd) * 4);
+  float gv[LPT], xq[LPT], a1[ADD1 ? LPT : 1], a2[ADD2 ? LPT : 1], a2q[A2M ? LPT : 1];
+  float sv[PART ? LPT : 1];
+  {
+    const auto gr = make_rsrc(dxt + off, pb), xr = make_rsrc(x0 + off, pb);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      gv[e] = bload(gr, uo + e * vstep, 0);
+      xq[e] = bload(xr, vo + e * vstep, 0);
+    }
+    if (ADD1) {
+      const auto ar = make_rsrc(add1 + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) a1[e] = bload(ar, vo + e * vstep, 0);
+    }
+    if (ADD2) {
+      const auto ar = make_rsrc(add2 + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) a2[e] = bload(ar, vo + e * vstep, 0);
+    }
+    if (A2M) {
+      const auto ar = make_rsrc(add2m + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) a2q[e] = bload(ar, vo + e * vstep, 0);
+    }
+    if (PART) {
+      const auto ar = make_rsrc(ps + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) sv[e] = bload(ar, vo + e * vstep, 0);
+    }
+  }
+  const float mu = m[us * C + c];
+  float pm = 0.f, pi = 0.f;
+  if (PART) { pm = pmean[c]; pi = pinvstd[c]; }
+  const auto dxr = make_rsrc(dx + off, pb);
+  float acc = 0.f, b0 = 0.f, b1 = 0.f;
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    float val = gv[e] * mu;
+    if (ADD1) val += a1[e];
+    if (ADD2) val += A2M ? (a2q[e] > 0.f ? a2[e] : 0.f) : a2[e];
+    bstore(dxr, val, vo + e * vstep, 0);
+    acc = fmaf(gv[e], xq[e], acc);   // past the plane both loads are 0
+    if (PART) {
+      const float g = xq[e] > 0.f ? val : 0.f;   // x0 = 0 past the plane
+      b0 += g;
+      b1 = fmaf(g, (sv[e] - pm) * pi, b1);
+    }
+  }
+  if (PART) {
+    block_sum2(b0, b1, red);
+    if (tid == 0) bn_part[plane] = make_float2(b0, b1);
+  }
+  s0[tid] = acc;
+  __syncthreads();
+  if (tid < V) {   // partial of source joint u = tid: its threads have v' = (u + c) mod V
+    int vq = tid + rc;
+    vq = vq >= V ? vq - V : vq;
+    float sum = 0.f;
+    for (int g = 0; g < GR; ++g) sum += s0[g * V + vq];
+    dmask_part[(size_t)plane * V + tid] = sum;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Shift_gcn input side, forward: shift_in gather + feature mask, materialised once
 // ------------------------------------------------------------------------------------
@@ -716,6 +943,14 @@ __global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_kernel(
 
 using namespace sgcn;
 
+// elements per thread of the plane-resident joint-aligned kernels on nt threads; 0 = the
+// plane does not fit (V > 64 or more than 32 per thread): the looping kernels take it
+int ja_lpt(int T, int V, int nt) {
+  if (V > 64) return 0;
+  const int ntj = (nt / V) * V, per = (T * V + ntj - 1) / ntj;
+  return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+}
+
 #define SGCN_PLANE_CHECK() \
   SGCN_REQUIRE(B >= 0 && C > 0 && T >= 0 && V > 0 && V <= kThreads)
 
@@ -780,6 +1015,59 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
   const int res = r == nullptr ? 0 : (rscale ? 2 : 1);
   dim3 g(B * C);
   float2* ys = (float2*)y_stats;
+  if (per_joint == 3) SGCN_REQUIRE(relu && !y_gathered);
+  {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
+    const int nt = T * V <= 4096 ? kThreads : 512;
+    const int lpt = ja_lpt(T, V, nt);
+    if (lpt) {
+      const int ox = ys ? 1 : (y_gathered ? 2 : 0);
+#define SGCN_AJ(NT, L, PJ, RS, RL, OX, ZU)                                                     \
+  bn_apply_ja_kernel<NT, L, PJ, RS, RL, OX, ZU><<<g, NT, 0, st>>>(                             \
+      x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V)
+#define SGCN_AJ_L(NT, PJ, RS, RL, OX, ZU)                                                      \
+  do {                                                                                         \
+    if (lpt == 8) SGCN_AJ(NT, 8, PJ, RS, RL, OX, ZU);                                          \
+    else if (lpt == 16) SGCN_AJ(NT, 16, PJ, RS, RL, OX, ZU);                                   \
+    else SGCN_AJ(NT, 32, PJ, RS, RL, OX, ZU);                                                  \
+  } while (0)
+#define SGCN_AJ_T(PJ, RS, RL, OX, ZU)                                                          \
+  do {                                                                                         \
+    if (nt == kThreads) SGCN_AJ_L(kThreads, PJ, RS, RL, OX, ZU);                               \
+    else SGCN_AJ_L(512, PJ, RS, RL, OX, ZU);                                                   \
+  } while (0)
+#define SGCN_AJ_O(PJ, RS, RL, ZU)                                                              \
+  do {                                                                                         \
+    if (ox == 1) SGCN_AJ_T(PJ, RS, RL, 1, ZU);                                                 \
+    else if (ox == 2) SGCN_AJ_T(PJ, RS, RL, 2, ZU);                                            \
+    else SGCN_AJ_T(PJ, RS, RL, 0, ZU);                                                         \
+  } while (0)
+      if (per_joint == 3) {
+        if (ys) {
+          if (res == 0) SGCN_AJ_T(true, 0, true, 1, true);
+          else if (res == 1) SGCN_AJ_T(true, 1, true, 1, true);
+          else SGCN_AJ_T(true, 2, true, 1, true);
+        } else {
+          if (res == 0) SGCN_AJ_T(true, 0, true, 0, true);
+          else if (res == 1) SGCN_AJ_T(true, 1, true, 0, true);
+          else SGCN_AJ_T(true, 2, true, 0, true);
+        }
+      } else if (relu) {
+        if (res == 0) SGCN_AJ_O(false, 0, true, false);
+        else if (res == 1) SGCN_AJ_O(false, 1, true, false);
+        else SGCN_AJ_O(false, 2, true, false);
+      } else {
+        if (res == 0) SGCN_AJ_O(false, 0, false, false);
+        else if (res == 1) SGCN_AJ_O(false, 1, false, false);
+        else SGCN_AJ_O(false, 2, false, false);
+      }
+#undef SGCN_AJ_O
+#undef SGCN_AJ_T
+#undef SGCN_AJ_L
+#undef SGCN_AJ
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
+  }
 #define SGCN_APPLY_X(PJ, RS, RL, OX)                                                        \
   bn_apply_kernel<PJ, RS, RL, OX><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale, rshift, y, \
                                                           ys, gather_m, y_gathered, C, T, V)
@@ -789,7 +1077,6 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
 #define SGCN_APPLY_R(PJ, RL) \
   if (res == 0) SGCN_APPLY(PJ, 0, RL); else if (res == 1) SGCN_APPLY(PJ, 1, RL); else SGCN_APPLY(PJ, 2, RL)
   if (per_joint == 3) {   // the Shift_gcn tail on the pre-shift_out contraction output
-    SGCN_REQUIRE(relu && !y_gathered);
 #define SGCN_APPLY_ZU(RS)                                                                      \
   (ys ? bn_apply_kernel<true, RS, true, 1, true><<<g, kThreads, 0, st>>>(                      \
             x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V)          \
@@ -880,6 +1167,41 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
   const int res = dr == nullptr ? 0 : (rcoef ? 2 : 1);
   const int F = per_joint ? C * V : C;
   dim3 g(B * C);
+  if (per_joint == 3) SGCN_REQUIRE(relu);
+  {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
+    const int nt = T * V <= 4096 ? kThreads : 512;
+    const int lpt = ja_lpt(T, V, nt);
+    if (lpt) {
+#define SGCN_BJ(NT, L, PJ, RL, RS)                                                             \
+  (dy_coef ? bn_bwd_apply_ja_kernel<NT, L, PJ, RL, RS, true><<<g, NT, 0, st>>>(                 \
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V)                     \
+           : bn_bwd_apply_ja_kernel<NT, L, PJ, RL, RS, false><<<g, NT, 0, st>>>(                \
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V))
+#define SGCN_BJ_L(NT, PJ, RL, RS)                                                              \
+  do {                                                                                         \
+    if (lpt == 8) SGCN_BJ(NT, 8, PJ, RL, RS);                                                  \
+    else if (lpt == 16) SGCN_BJ(NT, 16, PJ, RL, RS);                                           \
+    else SGCN_BJ(NT, 32, PJ, RL, RS);                                                          \
+  } while (0)
+#define SGCN_BJ_T(PJ, RL, RS)                                                                  \
+  do { if (nt == kThreads) SGCN_BJ_L(kThreads, PJ, RL, RS); else SGCN_BJ_L(512, PJ, RL, RS); } while (0)
+#define SGCN_BJ_R(PJ, RL)                                                                      \
+  do {                                                                                         \
+    if (res == 0) SGCN_BJ_T(PJ, RL, 0);                                                        \
+    else if (res == 1) SGCN_BJ_T(PJ, RL, 1);                                                   \
+    else SGCN_BJ_T(PJ, RL, 2);                                                                 \
+  } while (0)
+      if (per_joint == 3) SGCN_BJ_R(3, true);
+      else if (relu) SGCN_BJ_R(0, true);
+      else SGCN_BJ_R(0, false);
+#undef SGCN_BJ_R
+#undef SGCN_BJ_T
+#undef SGCN_BJ_L
+#undef SGCN_BJ
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
+  }
 #define SGCN_BA(PJ, RL, RS)                                                                   \
   (dy_coef ? bn_bwd_apply_kernel<PJ, RL, RS, true><<<g, kThreads, 0, st>>>(                      \
                  dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V)                      \
@@ -887,7 +1209,7 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                  dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V))
 #define SGCN_BA_R(PJ, RL) \
   if (res == 0) SGCN_BA(PJ, RL, 0); else if (res == 1) SGCN_BA(PJ, RL, 1); else SGCN_BA(PJ, RL, 2)
-  if (per_joint == 3) { SGCN_REQUIRE(relu); SGCN_BA_R(3, true); }
+  if (per_joint == 3) { SGCN_BA_R(3, true); }
   else if (relu) { SGCN_BA_R(0, true); } else { SGCN_BA_R(0, false); }
 #undef SGCN_BA_R
 #undef SGCN_BA
@@ -924,8 +1246,37 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
   SGCN_REQUIRE(!add2_mask || add2);
   hipStream_t st = (hipStream_t)stream;
   float2* pp = (float2*)prev_part;
+  if (add2_mask) SGCN_REQUIRE(add1);
+  {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
+    const int nt = T * V <= 4096 ? kThreads : 512;
+    const int lpt = ja_lpt(T, V, nt);
+    if (lpt) {
+#define SGCN_FJ(NT, L, A1, A2, PT, AM)                                                         \
+  gcn_dx_finish_ja_kernel<NT, L, A1, A2, PT, AM><<<B * C, NT, 0, st>>>(                        \
+      dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,     \
+      add2_mask)
+#define SGCN_FJ_L(NT, A1, A2, PT, AM)                                                          \
+  do {                                                                                         \
+    if (lpt == 8) SGCN_FJ(NT, 8, A1, A2, PT, AM);                                              \
+    else if (lpt == 16) SGCN_FJ(NT, 16, A1, A2, PT, AM);                                       \
+    else SGCN_FJ(NT, 32, A1, A2, PT, AM);                                                      \
+  } while (0)
+#define SGCN_FJ_T(A1, A2, PT, AM)                                                              \
+  do { if (nt == kThreads) SGCN_FJ_L(kThreads, A1, A2, PT, AM); else SGCN_FJ_L(512, A1, A2, PT, AM); } while (0)
+#define SGCN_FJ_P(A1, A2, AM)                                                                  \
+  do { if (pp) SGCN_FJ_T(A1, A2, true, AM); else SGCN_FJ_T(A1, A2, false, AM); } while (0)
+      if (add2_mask) SGCN_FJ_P(true, true, true);
+      else if (add1) { if (add2) SGCN_FJ_P(true, true, false); else SGCN_FJ_P(true, false, false); }
+      else { if (add2) SGCN_FJ_P(false, true, false); else SGCN_FJ_P(false, false, false); }
+#undef SGCN_FJ_P
+#undef SGCN_FJ_T
+#undef SGCN_FJ_L
+#undef SGCN_FJ
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if (add2_mask) {   // the identity-unit form: add1 given, add2 masked by add2_mask
-    SGCN_REQUIRE(add1);
     if (pp)
       gcn_dx_finish_kernel<true, true, true, true><<<B * C, kThreads, 0, st>>>(
           dxt, x0, m, add1, add2, dx, dmask_part, prev_s, prev_mean, prev_invstd, pp, C, T, V,
