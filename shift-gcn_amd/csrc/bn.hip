@@ -107,6 +107,61 @@ __device__ __forceinline__ int ref_feature(int f, int perm_V, int F) {
   return v * D + d;  // BatchNorm1d(V*C) feature index of (d, v)  (shift_gcn.py:135-137)
 }
 
+// Plane-resident form of moments_kernel (V <= 64, <= 32 elements per thread): the plane's
+// loads all in flight, dealt on the joint-aligned stride NTJ = (NT / V) * V (a thread's
+// joint is fixed: the per-joint sums stay in registers and are merged over the GR row
+// groups in fixed order). Same shifted sums (shift = the plane's / joint's first element).
+template <int NT, int LPT, bool PER_JOINT, bool ZU>
+__global__ __launch_bounds__(NT) void moments_ja_kernel(const float* __restrict__ x,
+                                                        float2* __restrict__ part, int T,
+                                                        int V, int C) {
+  __shared__ float s1[NT], s2[NT], red[2 * NT / 64];
+  const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see moments_kernel
+  const int GR = NT / V, NTJ = GR * V, tid = threadIdx.x;
+  const bool own = tid < NTJ;
+  const int w = tid % V;
+  const int P = T * V;
+  const float* __restrict__ xp = x + (size_t)plane * P;
+  const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
+  float xv[LPT];
+  {
+    const auto xr = make_rsrc(xp, (unsigned)P * 4u);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) xv[e] = bload(xr, vo + e * vstep, 0);
+  }
+  const int nval = own ? (P - tid + NTJ - 1) / NTJ : 0;   // this lane's elements e < nval
+  const float k0 = PER_JOINT ? xp[w] : xp[0];
+  float a = 0.f, q = 0.f;
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    const float d = e < nval ? xv[e] - k0 : 0.f;
+    a += d;
+    q += d * d;
+  }
+  if (PER_JOINT) {
+    s1[tid] = a;
+    s2[tid] = q;
+    __syncthreads();
+    if (tid < V) {
+      float ta = 0.f, tq = 0.f;
+      for (int g = 0; g < GR; ++g) { ta += s1[g * V + tid]; tq += s2[g * V + tid]; }
+      const float n = (float)T;
+      int wo = tid;
+      if (ZU) {
+        wo = tid + (plane % C) % V;
+        wo = wo >= V ? wo - V : wo;
+      }
+      part[(size_t)plane * V + wo] = make_float2(xp[tid] + ta / n, tq - ta * ta / n);
+    }
+  } else {
+    block_sum2(a, q, red);
+    if (tid == 0) {
+      const float n = (float)P;
+      part[plane] = make_float2(k0 + a / n, q - a * a / n);
+    }
+  }
+}
+
 // Per-feature sums over the batch of float2 partials: ONE WAVE PER FEATURE, the lanes
 // striding the batch (4 partials in flight per lane: one round trip for B <= 256), then a
 // fixed xor tree over the wave in double (deterministic). These kernels are pure latency
@@ -472,6 +527,85 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     block_sum2(a0, a1, red);
     if (RESBN) block_sum2(b0, b1, red);
     if (i == 0) {
+      part[plane] = make_float2(a0, a1);
+      if (RESBN) rpart[plane] = make_float2(b0, b1);
+    }
+  }
+}
+
+// Plane-resident form of bn_bwd_reduce_kernel (V <= 64, <= 32 elements per thread): the
+// plane's loads all in flight on the joint-aligned stride (a thread's joint is fixed:
+// per-joint statistics and the pre-rotation offset of x are per-thread constants).
+template <int NT, int LPT, bool PER_JOINT, bool RELU, bool RESBN, bool DYT>
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_ja_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ r, const float* __restrict__ rmean,
+    const float* __restrict__ rinvstd, const float* __restrict__ dyc, float2* __restrict__ part,
+    float2* __restrict__ rpart, int C, int T, int V) {
+  __shared__ float s0[NT], s1[NT], red[2 * NT / 64];
+  const int plane = blockIdx.x, c = plane % C;
+  const int GR = NT / V, NTJ = GR * V, tid = threadIdx.x;
+  const bool own = tid < NTJ;
+  const int w = tid % V;
+  const int P = T * V;
+  const size_t off = (size_t)plane * P;
+  const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
+  const unsigned pb = (unsigned)P * 4u;
+  int vx = w - c % V;   // in-row offset of this joint's (pre-rotation) x element
+  vx = vx < 0 ? vx + V : vx;
+  const unsigned xo = vo + (unsigned)((PER_JOINT ? vx - w : 0) * 4);
+  float gv[LPT], yv[RELU ? LPT : 1], xv[LPT], rv[RESBN ? LPT : 1];
+  {
+    const auto dyr = make_rsrc(dy + off, pb), xr = make_rsrc(x + off, pb);
+#pragma unroll
+    for (int e = 0; e < LPT; ++e) {
+      gv[e] = bload(dyr, vo + e * vstep, 0);
+      xv[e] = bload(xr, xo + e * vstep, 0);
+    }
+    if (RELU) {
+      const auto yr = make_rsrc(y + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) yv[e] = bload(yr, vo + e * vstep, 0);
+    }
+    if (RESBN) {
+      const auto rr = make_rsrc(r + off, pb);
+#pragma unroll
+      for (int e = 0; e < LPT; ++e) rv[e] = bload(rr, vo + e * vstep, 0);
+    }
+  }
+  float rm = 0.f, ri = 0.f, d1 = 1.f, d2 = 0.f, d3 = 0.f;
+  if (RESBN) { rm = rmean[c]; ri = rinvstd[c]; }
+  if (DYT) { d1 = dyc[c]; d2 = dyc[C + c]; d3 = dyc[2 * C + c]; }
+  const float mu = PER_JOINT ? mean[c * V + w] : mean[c];
+  const float is = PER_JOINT ? invstd[c * V + w] : invstd[c];
+  const int nval = own ? (P - tid + NTJ - 1) / NTJ : 0;   // this lane's elements e < nval
+  float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    float g = gv[e];
+    if (DYT) g = d1 * g + d2 * yv[e] + d3;
+    g = e < nval ? g : 0.f;
+    if (RELU) g = yv[e] > 0.f ? g : 0.f;
+    a0 += g;
+    a1 = fmaf(g, (xv[e] - mu) * is, a1);
+    if (RESBN) { b0 += g; b1 = fmaf(g, (rv[e] - rm) * ri, b1); }
+  }
+  if (PER_JOINT) {
+    if (RESBN) block_sum2(b0, b1, red);
+    s0[tid] = a0;
+    s1[tid] = a1;
+    __syncthreads();
+    if (tid < V) {
+      float t0 = 0.f, t1 = 0.f;
+      for (int g = 0; g < GR; ++g) { t0 += s0[g * V + tid]; t1 += s1[g * V + tid]; }
+      part[(size_t)plane * V + tid] = make_float2(t0, t1);
+    }
+    if (RESBN && tid == 0) rpart[plane] = make_float2(b0, b1);
+  } else {
+    block_sum2(a0, a1, red);
+    if (RESBN) block_sum2(b0, b1, red);
+    if (tid == 0) {
       part[plane] = make_float2(a0, a1);
       if (RESBN) rpart[plane] = make_float2(b0, b1);
     }
@@ -943,6 +1077,11 @@ __global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_kernel(
 
 using namespace sgcn;
 
+// largest plane the plane-resident kernels run on 256 threads (512 above): at NTU T = 300
+// (7,500 floats) 256 x 30 measured 0.8 % faster per step than 512 x 15 (same box,
+// profiles/r03_bnja/ab_moments_reduce_t256.txt)
+constexpr int kJaSplit = 8192;
+
 // elements per thread of the plane-resident joint-aligned kernels on nt threads; 0 = the
 // plane does not fit (V > 64 or more than 32 per thread): the looping kernels take it
 int ja_lpt(int T, int V, int nt) {
@@ -967,6 +1106,25 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
   SGCN_REQUIRE(x && part && T > 0);
   hipStream_t st = (hipStream_t)stream;
   SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
+  {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
+    const int nt = T * V <= kJaSplit ? kThreads : 512;
+    const int lpt = ja_lpt(T, V, nt);
+    if (lpt) {
+#define SGCN_MJ(NT, L, PJ)                                                                     \
+  moments_ja_kernel<NT, L, PJ, PJ><<<B * C, NT, 0, st>>>(x, (float2*)part, T, V, C)
+#define SGCN_MJ_L(NT, PJ)                                                                      \
+  do {                                                                                         \
+    if (lpt == 8) SGCN_MJ(NT, 8, PJ); else if (lpt == 16) SGCN_MJ(NT, 16, PJ);                 \
+    else SGCN_MJ(NT, 32, PJ);                                                                  \
+  } while (0)
+      if (nt == kThreads) { if (per_joint) SGCN_MJ_L(kThreads, true); else SGCN_MJ_L(kThreads, false); }
+      else { if (per_joint) SGCN_MJ_L(512, true); else SGCN_MJ_L(512, false); }
+#undef SGCN_MJ_L
+#undef SGCN_MJ
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if (per_joint == 3)
     moments_kernel<true, true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
   else moments_kernel<false><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
@@ -1017,7 +1175,7 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
   float2* ys = (float2*)y_stats;
   if (per_joint == 3) SGCN_REQUIRE(relu && !y_gathered);
   {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
-    const int nt = T * V <= 4096 ? kThreads : 512;
+    const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
       const int ox = ys ? 1 : (y_gathered ? 2 : 0);
@@ -1106,6 +1264,35 @@ int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x
   hipStream_t st = (hipStream_t)stream;
   dim3 g(B * C);
   const bool rb = r != nullptr;
+  if (per_joint == 3) SGCN_REQUIRE(relu);
+  {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
+    const int nt = T * V <= kJaSplit ? kThreads : 512;
+    const int lpt = ja_lpt(T, V, nt);
+    if (lpt) {
+#define SGCN_RJ(NT, L, PJ, RL, RB)                                                             \
+  (dy_coef ? bn_bwd_reduce_ja_kernel<NT, L, PJ, RL, RB, true><<<g, NT, 0, st>>>(                \
+                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,            \
+                 (float2*)rpart, C, T, V)                                                      \
+           : bn_bwd_reduce_ja_kernel<NT, L, PJ, RL, RB, false><<<g, NT, 0, st>>>(               \
+                 dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,            \
+                 (float2*)rpart, C, T, V))
+#define SGCN_RJ_L(NT, PJ, RL, RB)                                                              \
+  do {                                                                                         \
+    if (lpt == 8) SGCN_RJ(NT, 8, PJ, RL, RB); else if (lpt == 16) SGCN_RJ(NT, 16, PJ, RL, RB); \
+    else SGCN_RJ(NT, 32, PJ, RL, RB);                                                          \
+  } while (0)
+#define SGCN_RJ_T(PJ, RL, RB)                                                                  \
+  do { if (nt == kThreads) SGCN_RJ_L(kThreads, PJ, RL, RB); else SGCN_RJ_L(512, PJ, RL, RB); } while (0)
+      if (per_joint == 3) { if (rb) SGCN_RJ_T(true, true, true); else SGCN_RJ_T(true, true, false); }
+      else if (relu) { if (rb) SGCN_RJ_T(false, true, true); else SGCN_RJ_T(false, true, false); }
+      else { if (rb) SGCN_RJ_T(false, false, true); else SGCN_RJ_T(false, false, false); }
+#undef SGCN_RJ_T
+#undef SGCN_RJ_L
+#undef SGCN_RJ
+      SGCN_LAUNCH_CHECK();
+      return 0;
+    }
+  }
 #define SGCN_RED(PJ, RL, RB)                                                                \
   (dy_coef ? bn_bwd_reduce_kernel<PJ, RL, RB, true><<<g, kThreads, 0, st>>>(                   \
                  dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
@@ -1114,7 +1301,6 @@ int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x
                  dy, y, x, mean, invstd, r, rmean, rinvstd, dy_coef, (float2*)part,           \
                  (float2*)rpart, C, T, V))
   if (per_joint == 3) {   // x = the pre-shift_out contraction output (see the kernel)
-    SGCN_REQUIRE(relu);
     if (rb) SGCN_RED(true, true, true); else SGCN_RED(true, true, false);
   } else {
     if (relu) { if (rb) SGCN_RED(false, true, true); else SGCN_RED(false, true, false); }
@@ -1169,7 +1355,7 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
   dim3 g(B * C);
   if (per_joint == 3) SGCN_REQUIRE(relu);
   {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
-    const int nt = T * V <= 4096 ? kThreads : 512;
+    const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
 #define SGCN_BJ(NT, L, PJ, RL, RS)                                                             \
@@ -1248,7 +1434,7 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
   float2* pp = (float2*)prev_part;
   if (add2_mask) SGCN_REQUIRE(add1);
   {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
-    const int nt = T * V <= 4096 ? kThreads : 512;
+    const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
 #define SGCN_FJ(NT, L, A1, A2, PT, AM)                                                         \
