@@ -1014,6 +1014,12 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   a.a_bytes = (unsigned)((long long)M * K * 4);
   a.mask_bytes = mask ? (unsigned)(V * K * 4) : 0u;
   a.relu = rl ? 1 : 0;
+#ifdef SGCN_DIAG_X1B_BOUND
+  // timing diagnostic only (results wrong): temporal_linear's input-gradient contraction
+  // (W^T read m-contiguous, no bias / relu / accumulate) at M >= SGCN_DIAG_X1B_BOUND stores
+  // nothing, i.e. the dAs write a fused shift_in backward epilogue would never make
+  if (w_mcontig && !bias && !rl && !ac && M >= SGCN_DIAG_X1B_BOUND) a.y_bytes = 0;
+#endif
 #ifdef SGCN_DIAG_F2_BOUND
   // timing diagnostic only (tools/ab_variant.sh; results are wrong): the stride-2 residual
   // conv's read of the unit input is dropped by the range check, i.e. the most any fusion

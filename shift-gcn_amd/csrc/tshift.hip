@@ -942,6 +942,13 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
   const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u;
   const unsigned vstep = (unsigned)NTE * 4u, nbytes = (unsigned)n * 4u;
   const size_t poff = (size_t)plane * n;
+#ifdef SGCN_DIAG_X1B_BOUND
+  // timing diagnostic only (results wrong): the shift_in backward (affine taps) of a plane
+  // of C >= SGCN_DIAG_X1B_BOUND channels reads no gout (the dAs read a fused epilogue saves)
+  const unsigned gbytes = AFFINE && !GP && C >= SGCN_DIAG_X1B_BOUND ? 0u : nbytes;
+#else
+  const unsigned gbytes = nbytes;
+#endif
   float t[LPT], rin_r[LPT];
   float zr[GBN ? LPT : 1];
   {   // every global load of the plane in flight together
@@ -963,7 +970,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
 #pragma unroll
       for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
     } else {
-      const auto gr = make_rsrc(gout + poff, nbytes);
+      const auto gr = make_rsrc(gout + poff, gbytes);
 #pragma unroll
       for (int e = 0; e < LPT; ++e) {
         t[e] = bload(gr, vo + e * vstep, 0);
@@ -1559,6 +1566,8 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
   (void)ypos_is_raw;   // stride 1: the +0.5 of shift.py:17-18 never applies
   hipStream_t st = (hipStream_t)stream;
   float2* pg = (float2*)ws;
+  // 512 threads above 4K-float planes: 256 threads at NTU T = 300 measured 0.3 % slower per
+  // step (profiles/r03_x1b/ab_x1b_bound.txt, variant bnin256)
   const int ntb = H * W <= 4096 ? 256 : 512;
   const bool ok = launch_ra<false, true, false, true, false>(
       ntb, nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, B, C,
