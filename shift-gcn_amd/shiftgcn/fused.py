@@ -586,10 +586,13 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
 # ======================================================================================
 # Shift_tcn's shift_in fused into temporal_linear's operand staging (sgcn_pw_fwd_tshift)
 # from this many input channels up; below, the two-launch form (shift launch + contraction).
-# With the weight gradients on the side stream, fusing the C = 128 units costs 0.3 % of the
-# step and the C = 256 units are neutral (same-box A/B, profiles/r02_close/
-# ab_tshift_fusion.txt). A/B knob (a value above 256 turns the fusion off).
-TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "256"))
+# On gfx950 the fp32 MFMA shares the VALU issue, so the fused operand's per-element tap
+# arithmetic comes out of the MFMA budget: with the weight gradients on the side stream
+# fusing the C = 128 units cost 0.3 % and C = 256 was neutral (round 2,
+# profiles/r02_close/ab_tshift_fusion.txt); since the padded shift kernel (round 3) the
+# two-launch form is faster at C = 256 too (+0.5 % same-box, profiles/r03_tsh/), so by
+# default no unit fuses (512 exceeds every Shift-GCN width). A/B knob (0 = every unit).
+TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "512"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
 # (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass. A/B knob.
 GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
