@@ -41,14 +41,14 @@ def short(n):
 OP_CLASSES = {
     "pw_fwd": (("pwg_fwd_kernel",), ("tshift_params_kernel",)),
     "pw_dw": (("pw_dw_kernel", "pw_dw3_kernel"), ("slab_reduce_kernel",)),
-    "tshift_fwd": (("tshift_fwd_kernel", "tshift_fwd_lds_kernel", "tshift_fwd_pre_kernel",
-                    "tshift_fwd_tail_kernel"), ()),
-    "tshift_bwd": (("tshift_bwd_kernel", "tshift_bwd_lds_kernel"), ()),
-    "bn_stats": (("moments_kernel",), ()),
-    "bn_apply": (("bn_apply_kernel",), ()),
-    "bn_bwd_reduce": (("bn_bwd_reduce_kernel",), ()),
-    "bn_bwd_apply": (("bn_bwd_apply_kernel",), ()),
-    "gcn_dx_finish": (("gcn_dx_finish_kernel",), ()),
+    "tshift_fwd": (("tshift_fwd_kernel", "tshift_fwd_lds_kernel", "tshift_fwd_pad_kernel",
+                    "tshift_fwd_pre_kernel", "tshift_fwd_tail_kernel"), ()),
+    "tshift_bwd": (("tshift_bwd_kernel", "tshift_bwd_ra_kernel", "tshift_bwd_s2_kernel"), ()),
+    "bn_stats": (("moments_kernel", "moments_ja_kernel"), ()),
+    "bn_apply": (("bn_apply_kernel", "bn_apply_ja_kernel"), ()),
+    "bn_bwd_reduce": (("bn_bwd_reduce_kernel", "bn_bwd_reduce_ja_kernel"), ()),
+    "bn_bwd_apply": (("bn_bwd_apply_kernel", "bn_bwd_apply_ja_kernel"), ()),
+    "gcn_dx_finish": (("gcn_dx_finish_kernel", "gcn_dx_finish_ja_kernel"), ()),
     "gcn_gather": (("gcn_gather_kernel",), ()),
     "finalize": (("bn_finalize_kernel", "bn_eval_coef_kernel", "bn_bwd_finalize_kernel",
                   "bn_bwd_finalize_gbn_kernel", "mask_prep_kernel", "mask_grad_finalize_kernel",
