@@ -22,11 +22,13 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 19
+#define SGCN_ABI_VERSION 20
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). 19: the measured-and-rejected
  * variants are gone (the S-free unit tail's statistics-only shift and re-formed bn2 input,
- * the re-forming temporal-shift weight gradient, per_joint = 1 / 2 rotated-store layouts). */
+ * the re-forming temporal-shift weight gradient, per_joint = 1 / 2 rotated-store layouts).
+ * 20: sgcn_tshift_bwd_gbn also takes the down conv's BatchNorm (d, d_mean, d_invstd,
+ * d_part; NULL when the Shift_gcn has none). */
 int sgcn_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
@@ -145,6 +147,11 @@ int sgcn_tshift_bwd_f64(const double* gout, const double* in, const double* xpos
  * stored it BEFORE its shift_out (per_joint = 3 layout: logical joint w at (w - c) mod W),
  * statistics in the per-joint local order. Feed z_part to
  * sgcn_bn_bwd_finalize_gbn; no separate sgcn_bn_bwd_reduce pass over (gin, in, z).
+ * d (optional, with d_mean/d_invstd/d_part; ABI 20): a Shift_gcn WITH a down conv, whose
+ * BatchNorm2d output is added before the ReLU (in = relu(bn(z) + bnd(d))): d_part[j][b*C + c]
+ * = the same six sums over the plane with zh replaced by dh = (d - d_mean[c]) * d_invstd[c]
+ * (d in the natural layout), finalized by sgcn_bn_bwd_finalize_gbn with V = 1 — the down
+ * BatchNorm's backward sums without a reduce pass either.
  * H*W <= 16384, W <= 64 and at most 32 elements per thread of the joint-aligned stride
  * (NT / W) * W, NT = 256 (H*W <= 8192; 512 if 256 would need more than 32) or 512 (else
  * SGCN_EINVAL: use sgcn_tshift_bwd + sgcn_bn_bwd_reduce). */
@@ -152,8 +159,9 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
                         const float* ypos, const float* in_scale, const float* in_shift,
                         const float* bn_mean, const float* bn_invstd, float* bn_part,
                         const float* z, const float* z_mean, const float* z_invstd,
-                        float* z_part, float* gin, float* gx, float* gy, void* ws,
-                        size_t ws_bytes, int B, int C, int H, int W, void* stream);
+                        float* z_part, const float* d, const float* d_mean,
+                        const float* d_invstd, float* d_part, float* gin, float* gx, float* gy,
+                        void* ws, size_t ws_bytes, int B, int C, int H, int W, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Pointwise (1x1) channel contraction with the joint-shift gathers fused (fp32 MFMA)

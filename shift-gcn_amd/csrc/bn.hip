@@ -1087,7 +1087,7 @@ constexpr int kJaSplit = 8192;
 int ja_lpt(int T, int V, int nt) {
   if (V > 64) return 0;
   const int ntj = (nt / V) * V, per = (T * V + ntj - 1) / ntj;
-  return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+  return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 24 ? 24 : (per <= 32 ? 32 : 0)));
 }
 
 #define SGCN_PLANE_CHECK() \
@@ -1115,6 +1115,7 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
 #define SGCN_MJ_L(NT, PJ)                                                                      \
   do {                                                                                         \
     if (lpt == 8) SGCN_MJ(NT, 8, PJ); else if (lpt == 16) SGCN_MJ(NT, 16, PJ);                 \
+    else if (lpt == 24) SGCN_MJ(NT, 24, PJ);                                                   \
     else SGCN_MJ(NT, 32, PJ);                                                                  \
   } while (0)
       if (nt == kThreads) { if (per_joint) SGCN_MJ_L(kThreads, true); else SGCN_MJ_L(kThreads, false); }
@@ -1186,6 +1187,7 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
   do {                                                                                         \
     if (lpt == 8) SGCN_AJ(NT, 8, PJ, RS, RL, OX, ZU);                                          \
     else if (lpt == 16) SGCN_AJ(NT, 16, PJ, RS, RL, OX, ZU);                                   \
+    else if (lpt == 24) SGCN_AJ(NT, 24, PJ, RS, RL, OX, ZU);                                   \
     else SGCN_AJ(NT, 32, PJ, RS, RL, OX, ZU);                                                  \
   } while (0)
 #define SGCN_AJ_T(PJ, RS, RL, OX, ZU)                                                          \
@@ -1279,6 +1281,7 @@ int sgcn_bn_bwd_reduce(const float* dy, const float* y, int relu, const float* x
 #define SGCN_RJ_L(NT, PJ, RL, RB)                                                              \
   do {                                                                                         \
     if (lpt == 8) SGCN_RJ(NT, 8, PJ, RL, RB); else if (lpt == 16) SGCN_RJ(NT, 16, PJ, RL, RB); \
+    else if (lpt == 24) SGCN_RJ(NT, 24, PJ, RL, RB);                                           \
     else SGCN_RJ(NT, 32, PJ, RL, RB);                                                          \
   } while (0)
 #define SGCN_RJ_T(PJ, RL, RB)                                                                  \
@@ -1367,6 +1370,7 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
   do {                                                                                         \
     if (lpt == 8) SGCN_BJ(NT, 8, PJ, RL, RS);                                                  \
     else if (lpt == 16) SGCN_BJ(NT, 16, PJ, RL, RS);                                           \
+    else if (lpt == 24) SGCN_BJ(NT, 24, PJ, RL, RS);                                           \
     else SGCN_BJ(NT, 32, PJ, RL, RS);                                                          \
   } while (0)
 #define SGCN_BJ_T(PJ, RL, RS)                                                                  \
@@ -1445,6 +1449,7 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
   do {                                                                                         \
     if (lpt == 8) SGCN_FJ(NT, 8, A1, A2, PT, AM);                                              \
     else if (lpt == 16) SGCN_FJ(NT, 16, A1, A2, PT, AM);                                       \
+    else if (lpt == 24) SGCN_FJ(NT, 24, A1, A2, PT, AM);                                       \
     else SGCN_FJ(NT, 32, A1, A2, PT, AM);                                                      \
   } while (0)
 #define SGCN_FJ_T(A1, A2, PT, AM)                                                              \

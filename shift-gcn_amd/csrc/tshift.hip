@@ -916,7 +916,14 @@ __global__ __launch_bounds__(NT) void tshift_bwd_s2_kernel(
 // Shift_tcn.bn's mean mu (k2*H + k3 = k2*(H - mu) + (k3 + k2*mu), no cancellation):
 //   {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh} over t where H > 0,
 //   zh = (Z - zmean[c,v]) * zinvstd[c,v]; sgcn_bn_bwd_finalize_gbn combines them.
-template <int NT, int LPT, bool AFFINE, bool RELU_MASK, bool BNP, bool GP, bool GBN>
+// GBD (with GBN: the Shift_gcn HAS a down conv, whose BatchNorm2d output d is added before
+// the ReLU: H = relu(bn(Z) + bnd(d)), shift_gcn.py:140-141): also the plane sums of that
+// BatchNorm's backward, {sum dA, sum (H-mu), sum 1, sum dA*dh, sum (H-mu)*dh, sum dh} over
+// H > 0, dh = (d - d_mean[c]) * d_invstd[c], to gdpart[j][plane] — the same six-sum form,
+// finalized by sgcn_bn_bwd_finalize_gbn with V = 1 — so no sgcn_bn_bwd_reduce pass over
+// (dA, H, Z, d) remains for the units with a down conv either.
+template <int NT, int LPT, bool AFFINE, bool RELU_MASK, bool BNP, bool GP, bool GBN,
+          bool GBD = false>
 __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
     const float* __restrict__ gout, const float* __restrict__ in,
     const float* __restrict__ xpos, const float* __restrict__ ypos,
@@ -926,8 +933,11 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
     int H, int W, const float* __restrict__ gdy, const float* __restrict__ gy,
     const float* __restrict__ gx, const float* __restrict__ gcoef,
     const float* __restrict__ gz, const float* __restrict__ gzm,
-    const float* __restrict__ gzi, float* __restrict__ gzpart) {
+    const float* __restrict__ gzi, float* __restrict__ gzpart, const float* __restrict__ gd = nullptr,
+    const float* __restrict__ gdm = nullptr, const float* __restrict__ gdi = nullptr,
+    float* __restrict__ gdpart = nullptr) {
   static_assert(!GBN || (AFFINE && BNP && !GP), "GBN: shift_in with BNP");
+  static_assert(!GBD || GBN, "GBD extends GBN");
   extern __shared__ float lds[];   // [(H + 2*kPadRows) * WP] padded gout (GBN: >= 6*NT)
   __shared__ float red[4 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
@@ -950,7 +960,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
   const unsigned gbytes = nbytes;
 #endif
   float t[LPT], rin_r[LPT];
-  float zr[GBN ? LPT : 1];
+  float zr[GBN ? LPT : 1], dr[GBD ? LPT : 1];
   {   // every global load of the plane in flight together
     const auto inr = make_rsrc(in + poff, nbytes);
     if (GP) {
@@ -986,6 +996,11 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
 #pragma unroll
         for (int e = 0; e < LPT; ++e) zr[e] = bload(zrr, zo + e * vstep, 0);
       }
+      if (GBD) {   // the down conv output: natural layout, the element's own address
+        const auto drr = make_rsrc(gd + poff, nbytes);
+#pragma unroll
+        for (int e = 0; e < LPT; ++e) dr[e] = bload(drr, vo + e * vstep, 0);
+      }
     }
   }
   zero_pad<NT>(lds, H, W);
@@ -1001,8 +1016,9 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
   const float x = xpos[c], y = ypos[c];
   float a = 1.f, b = 0.f;
   if (AFFINE) { a = scale[c]; b = shift[c]; }
-  float zm = 0.f, zi = 0.f;
+  float zm = 0.f, zi = 0.f, dmu = 0.f, dis = 0.f;
   if (GBN) { zm = gzm[c * W + w]; zi = gzi[c * W + w]; }
+  if (GBD) { dmu = gdm[c]; dis = gdi[c]; }
   __syncthreads();
 
   // input-gradient taps: gout at (h + r.y1 + {0,1}, w + r.x1 + {0,1}) (.cu:108-150);
@@ -1018,6 +1034,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
   const auto gir = make_rsrc(gin + poff, nbytes);
   float bs0 = 0.f, bs1 = 0.f, ax = 0.f, ay = 0.f;
   float a6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // GBN per-joint sums
+  float d6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // GBD plane sums
   // one element: value, stores and sums from its eight taps (tail: the element may lie
   // past the plane — its load returned 0, its store drops, its sums are masked here)
   auto elem = [&](int e, bool tail, float q11, float q21, float q12, float q22, float G11,
@@ -1041,6 +1058,15 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
       a6[3] = fmaf(vv, zh, a6[3]);
       a6[4] = fmaf(hc, zh, a6[4]);
       a6[5] += zh;
+      if (GBD) {
+        const float dh = act ? (dr[e] - dmu) * dis : 0.f;
+        d6[0] += vv;
+        d6[1] += hc;
+        d6[2] += act ? 1.f : 0.f;
+        d6[3] = fmaf(vv, dh, d6[3]);
+        d6[4] = fmaf(hc, dh, d6[4]);
+        d6[5] += dh;
+      }
     }
     if (BNP) {
       bs0 += val;
@@ -1099,9 +1125,18 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
         a6[0] += val;
         a6[1] += hc;
         a6[2] += 1.f;
-        a6[3] += val * zh;
-        a6[4] += hc * zh;
+        a6[3] = fmaf(val, zh, a6[3]);
+        a6[4] = fmaf(hc, zh, a6[4]);
         a6[5] += zh;
+        if (GBD) {
+          const float dh = (bload(make_rsrc(gd + poff, nbytes), vo + e * vstep, 0) - dmu) * dis;
+          d6[0] += val;
+          d6[1] += hc;
+          d6[2] += 1.f;
+          d6[3] = fmaf(val, dh, d6[3]);
+          d6[4] = fmaf(hc, dh, d6[4]);
+          d6[5] += dh;
+        }
       }
       if (BNP) {
         bs0 += val;
@@ -1126,6 +1161,15 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
   } else {
     block_sum2(ax, ay, red);
     if (tid == 0) pgrad[plane] = make_float2(ax, ay);
+  }
+  if (GBD) {   // the down BatchNorm's six plane sums
+    block_sum4(d6[0], d6[1], d6[2], d6[3], red);
+    block_sum2(d6[4], d6[5], red);
+    if (tid == 0) {
+      const size_t np = gridDim.x;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) gdpart[k * np + plane] = d6[k];
+    }
   }
   if (GBN) {
     // merge the GR row groups of each joint in fixed order (deterministic)
@@ -1232,7 +1276,7 @@ void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const 
 int pad_fwd_lpt(int H, int W, int nt) {
   if (W > 64) return 0;
   const int ntj = (nt / W) * W, per = (H * W + ntj - 1) / ntj;
-  const int lpt = per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+  const int lpt = per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 24 ? 24 : (per <= 32 ? 32 : 0)));
   return (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float) > 65536 ? 0 : lpt;
 }
 
@@ -1255,7 +1299,7 @@ bool launch_fwd_pad(bool affine, bool stats, const float* in, float* out, const 
     if (affine) { if (stats) SGCN_FWDP(L, true, true); else SGCN_FWDP(L, true, false); }     \
     else { if (stats) SGCN_FWDP(L, false, true); else SGCN_FWDP(L, false, false); }          \
   } while (0)
-  if (lpt == 8) SGCN_FWDP_AS(8); else if (lpt == 16) SGCN_FWDP_AS(16); else SGCN_FWDP_AS(32);
+  if (lpt == 8) SGCN_FWDP_AS(8); else if (lpt == 16) SGCN_FWDP_AS(16); else if (lpt == 24) SGCN_FWDP_AS(24); else SGCN_FWDP_AS(32);
 #undef SGCN_FWDP_AS
 #undef SGCN_FWDP
   return true;
@@ -1327,7 +1371,7 @@ int ra_lpt(int n, int nt, int W) {
   const int nte = (nt / W) * W;
   if (nte <= 0 || W > 64) return 0;
   const int per = (n + nte - 1) / nte;
-  return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 32 ? 32 : 0));
+  return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 24 ? 24 : (per <= 32 ? 32 : 0)));
 }
 
 // largest stride-1 plane the joint-aligned backward kernels with affine taps (shift_in:
@@ -1345,24 +1389,25 @@ constexpr size_t kRaLdsMax = 65536;
 
 // launch tshift_bwd_ra_kernel on nt threads (256 or 512) with LPT = ra_lpt(H*W, nt, W);
 // returns false (nothing launched) when the plane does not fit its LDS or registers
-template <bool AFFINE, bool RELU, bool BNP, bool GP, bool GBN>
+template <bool AFFINE, bool RELU, bool BNP, bool GP, bool GBN, bool GBD = false>
 bool launch_ra(int nt, const float* gout, const float* in, const float* xpos,
                const float* ypos, const float* scale, const float* shift, const float* bmu,
                const float* bis, float* gin, float2* pg, float2* bp, int B, int C, int H,
                int W, const float* gdy, const float* gy, const float* gx, const float* gcoef,
                const float* gz, const float* gzm, const float* gzi, float* gzpart,
-               hipStream_t st) {
+               hipStream_t st, const float* gd = nullptr, const float* gdm = nullptr,
+               const float* gdi = nullptr, float* gdpart = nullptr) {
   const int lpt = ra_lpt(H * W, nt, W);
   const size_t lds = ra_lds_bytes(H, W, nt, GBN);
   if (lpt == 0 || lds > kRaLdsMax) return false;
 #define SGCN_RA(NT, L)                                                                         \
-  tshift_bwd_ra_kernel<NT, L, AFFINE, RELU, BNP, GP, GBN><<<B * C, NT, lds, st>>>(             \
+  tshift_bwd_ra_kernel<NT, L, AFFINE, RELU, BNP, GP, GBN, GBD><<<B * C, NT, lds, st>>>(        \
       gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, gdy, gy, gx, gcoef,  \
-      gz, gzm, gzi, gzpart)
+      gz, gzm, gzi, gzpart, gd, gdm, gdi, gdpart)
   if (nt == 256) {
-    if (lpt == 8) SGCN_RA(256, 8); else if (lpt == 16) SGCN_RA(256, 16); else SGCN_RA(256, 32);
+    if (lpt == 8) SGCN_RA(256, 8); else if (lpt == 16) SGCN_RA(256, 16); else if (lpt == 24) SGCN_RA(256, 24); else SGCN_RA(256, 32);
   } else {
-    if (lpt == 8) SGCN_RA(512, 8); else if (lpt == 16) SGCN_RA(512, 16); else SGCN_RA(512, 32);
+    if (lpt == 8) SGCN_RA(512, 8); else if (lpt == 16) SGCN_RA(512, 16); else if (lpt == 24) SGCN_RA(512, 24); else SGCN_RA(512, 32);
   }
 #undef SGCN_RA
   return true;
@@ -1451,9 +1496,9 @@ int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const flo
 #define SGCN_PREP_R(NT, L) \
   do { if (r_scale) SGCN_PREP(NT, L, 2); else SGCN_PREP(NT, L, 1); } while (0)
       if (nt == kThreads) {
-        if (lpt == 8) SGCN_PREP_R(kThreads, 8); else if (lpt == 16) SGCN_PREP_R(kThreads, 16); else SGCN_PREP_R(kThreads, 32);
+        if (lpt == 8) SGCN_PREP_R(kThreads, 8); else if (lpt == 16) SGCN_PREP_R(kThreads, 16); else if (lpt == 24) SGCN_PREP_R(kThreads, 24); else SGCN_PREP_R(kThreads, 32);
       } else {
-        if (lpt == 8) SGCN_PREP_R(512, 8); else if (lpt == 16) SGCN_PREP_R(512, 16); else SGCN_PREP_R(512, 32);
+        if (lpt == 8) SGCN_PREP_R(512, 8); else if (lpt == 16) SGCN_PREP_R(512, 16); else if (lpt == 24) SGCN_PREP_R(512, 24); else SGCN_PREP_R(512, 32);
       }
 #undef SGCN_PREP_R
 #undef SGCN_PREP
@@ -1517,9 +1562,9 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
     else { if (go) SGCN_TAILP(NT, L, 2, true); else SGCN_TAILP(NT, L, 2, false); }             \
   } while (0)
       if (nt == kThreads) {
-        if (lpt == 8) SGCN_TAILP_RG(kThreads, 8); else if (lpt == 16) SGCN_TAILP_RG(kThreads, 16); else SGCN_TAILP_RG(kThreads, 32);
+        if (lpt == 8) SGCN_TAILP_RG(kThreads, 8); else if (lpt == 16) SGCN_TAILP_RG(kThreads, 16); else if (lpt == 24) SGCN_TAILP_RG(kThreads, 24); else SGCN_TAILP_RG(kThreads, 32);
       } else {
-        if (lpt == 8) SGCN_TAILP_RG(512, 8); else if (lpt == 16) SGCN_TAILP_RG(512, 16); else SGCN_TAILP_RG(512, 32);
+        if (lpt == 8) SGCN_TAILP_RG(512, 8); else if (lpt == 16) SGCN_TAILP_RG(512, 16); else if (lpt == 24) SGCN_TAILP_RG(512, 24); else SGCN_TAILP_RG(512, 32);
       }
 #undef SGCN_TAILP_RG
 #undef SGCN_TAILP
@@ -1593,9 +1638,11 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
                         const float* ypos, const float* in_scale, const float* in_shift,
                         const float* bn_mean, const float* bn_invstd, float* bn_part,
                         const float* z, const float* z_mean, const float* z_invstd,
-                        float* z_part, float* gin, float* gx, float* gy, void* ws,
-                        size_t ws_bytes, int B, int C, int H, int W, void* stream) {
+                        float* z_part, const float* d, const float* d_mean,
+                        const float* d_invstd, float* d_part, float* gin, float* gx, float* gy,
+                        void* ws, size_t ws_bytes, int B, int C, int H, int W, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && W <= 64);
+  SGCN_REQUIRE((d == nullptr) == (d_part == nullptr) && (!d || (d_mean && d_invstd)));
   SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
   SGCN_REQUIRE(gout && in && xpos && ypos && in_scale && in_shift && bn_mean && bn_invstd &&
                bn_part && z && z_mean && z_invstd && z_part && gin && ws);
@@ -1609,9 +1656,14 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   // stride (NT / W) * W; 512 threads when 256 would need more than 32 per thread
   const int n = H * W;
   const int ntg = n <= kRaSplit256 && ra_lpt(n, 256, W) ? 256 : kBwdThreads;
-  const bool ok = launch_ra<true, false, true, false, true>(
-      ntg, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B, C, H,
-      W, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part, st);
+  const bool ok =
+      d ? launch_ra<true, false, true, false, true, true>(
+              ntg, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B,
+              C, H, W, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part, st, d,
+              d_mean, d_invstd, d_part)
+        : launch_ra<true, false, true, false, true>(
+              ntg, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B,
+              C, H, W, nullptr, nullptr, nullptr, nullptr, z, z_mean, z_invstd, z_part, st);
   SGCN_REQUIRE(ok);   // within the largest LPT and 64 KiB of LDS (ops.ra_fits)
   SGCN_LAUNCH_CHECK();
   if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # same-box A/B of two builds (tuning only, e.g. tools/ab_lib.sh): another in-tree build of
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
-ABI_VERSION = 19
+ABI_VERSION = 20
 EINVAL = -22
 
 _lib = None
@@ -73,7 +73,7 @@ SIGNATURES = {
     "sgcn_mask_grad_finalize": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "sgcn_modalities": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "sgcn_tshift_bwd_gbn": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                 _P, _Z, _I, _I, _I, _I, _P]),
+                                 _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _P]),
     "sgcn_bn_bwd_finalize_gbn": (_I, [_P, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _I,
                                       _P, _P]),
     "sgcn_head_ws_bytes": (_Z, [_I, _I, _I, _I]),

@@ -180,8 +180,9 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     B, Cin, T, V = x0.shape
     Cout = mod.out_channels
     g = {}
+    rpart = None
     if pre6 is not None:
-        assert dy_coef is not None and not mod.has_down
+        assert dy_coef is not None and (pre6[2] is not None) == mod.has_down
         coefZ, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize_gbn(
             pre6[0], B, Cout, V, B * T, dy_coef, pre6[1], s.zst, mod.bn)
     else:
@@ -197,8 +198,12 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     g_id = dD0 = None
     if mod.has_down:
         conv, bnd = mod.down[0], mod.down[1]
-        coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
-            rpart, B, Cout, B * T * V, s.dst, bnd)
+        if pre6 is not None:   # the down BatchNorm's six plane sums, from the same launch
+            coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize_gbn(
+                pre6[2], B, Cout, 1, B * T * V, dy_coef, pre6[1], s.dst, bnd)
+        else:
+            coefD, g["down.1.weight"], g["down.1.bias"] = ops.bn_bwd_finalize(
+                rpart, B, Cout, B * T * V, s.dst, bnd)
         dD0 = _empty(B, Cout, T, V, like=x0)
         ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 3, r=s.D0, rcoef=coefD, dr=dD0, dx=dZ,
                          dy_coef=dy_coef)
@@ -324,8 +329,9 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
                       out=None, off=False):
     """dS: gradient w.r.t. S (pre-bn2). Returns (dH, grads), or ((dA, coef), grads) with
     ``materialize_dx=False`` (dH = coef[0]*dA + coef[1]*H + coef[2], fused downstream).
-    ``gcn_z`` = (Z, zst) of the producing Shift_gcn (no down conv): its BatchNorm's
-    backward sums come out of the shift_in backward launch, returned as out["pre6"]."""
+    ``gcn_z`` = (Z, zst[, (D0, dst)]) of the producing Shift_gcn: its BatchNorm's (and its
+    down BatchNorm's) backward sums come out of the shift_in backward launch, returned as
+    out["pre6"] = (z sums, Shift_tcn.bn stats, down sums or None)."""
     H = s.H
     B, C, T, V = H.shape
     Cout = mod.out_channels
@@ -352,10 +358,11 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
     # the Shift_gcn BatchNorm that produced H)
     if gcn_z is not None and GBN_FUSION and si.stride == 1 and ops.ra_fits(T * V, V):
-        dA, gx, gy, part, zpart = ops.tshift_bwd_gbn(
-            dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0], gcn_z[1],
-            defer_pos=off)
-        out["pre6"] = (zpart, s.ast)
+        down = gcn_z[2] if len(gcn_z) > 2 else None
+        res = ops.tshift_bwd_gbn(dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0],
+                                 gcn_z[1], defer_pos=off, down=down)
+        dA, gx, gy, part, zpart = res[:5]
+        out["pre6"] = (zpart, s.ast, res[5] if down is not None else None)
     else:
         dA, gx, gy, part = ops.tshift_bwd(
             dAs, H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=s.ast.scale,
@@ -486,10 +493,12 @@ def unit_forward(unit, x, training):
 
 
 def _gcn_z(unit, s: UnitSaved):
-    """(Z, zst) of the unit's Shift_gcn when its BatchNorm's backward sums can come out of
-    the shift_in backward launch (no down conv: its BN would need another input)."""
-    # (sgcn_tshift_bwd_gbn reads Z in the pre-shift_out layout)
-    return None if unit.gcn1.has_down else (s.gs.Z, s.gs.zst)
+    """(Z, zst[, (D0, dst)]) of the unit's Shift_gcn: its BatchNorm's backward sums (and,
+    with a down conv, the down BatchNorm's) come out of the shift_in backward launch."""
+    # (sgcn_tshift_bwd_gbn reads Z in the pre-shift_out layout, D0 in the natural one)
+    if unit.gcn1.has_down:
+        return (s.gs.Z, s.gs.zst, (s.gs.D0, s.gs.dst)) if GBN_FUSION >= 2 else None
+    return (s.gs.Z, s.gs.zst)
 
 
 def _off_path_ok(unit, s: UnitSaved):
@@ -594,8 +603,10 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
 # default no unit fuses (512 exceeds every Shift-GCN width). A/B knob (0 = every unit).
 TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "512"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
-# (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass. A/B knob.
-GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "1"))
+# (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass: 2 = every unit (with a
+# down conv, the down BatchNorm's sums too; round 3), 1 = units without a down conv only
+# (round 2), 0 = off. A/B knob.
+GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "2"))
 # Off-critical-path launches of linked units on a side stream (_OffPath): the weight-
 # gradient contractions (after the dX contraction of the same operand), the position-
 # gradient finalizes, the next unit's mask and the forward's down / residual conv branches.

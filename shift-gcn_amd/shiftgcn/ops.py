@@ -306,14 +306,19 @@ def ra_fits(n, V):
     return -(-n // ((nt // V) * V)) <= 32
 
 
-def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats", defer_pos=False):
+def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats", defer_pos=False,
+                   down=None):
     """Shift_tcn.shift_in backward (stride 1, Shift_tcn.bn's affine on the taps and its
     backward partials) that also emits the k-free backward sums of Shift_gcn.bn, whose
-    input is ``z`` and whose ReLU output is ``inp`` (sgcn_tshift_bwd_gbn). Returns
-    (grad_input, grad_xpos, grad_ypos, bn_part, z_part6)."""
+    input is ``z`` and whose ReLU output is ``inp`` (sgcn_tshift_bwd_gbn). ``down`` =
+    (d, d_stats): the Shift_gcn's down conv output and its BatchNorm's statistics — the
+    six plane sums of that BatchNorm's backward come out of the same launch. Returns
+    (grad_input, grad_xpos, grad_ypos, bn_part, z_part6[, d_part6])."""
     check_input(gout, "grad_output")
     check_input(inp, "input")
     check_input(z, "z")
+    if down is not None:
+        check_input(down[0], "d")
     B, C, H, W = inp.shape
     lib = _lib.load()
     dev = inp.device
@@ -323,14 +328,23 @@ def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats", defe
     gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
     bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32)
     zpart = torch.empty((6 * B * C * W,), device=dev, dtype=_F32)
-    nb = 4 * (gout.numel() + 3 * inp.numel())
-    with _timed("tshift_bwd", 0, nb, inp, "GBN " + _shp(inp)):
+    d, dst, dpart = None, None, None
+    if down is not None:
+        d, dst = down
+        dpart = torch.empty((6 * B * C,), device=dev, dtype=_F32)
+    nb = 4 * (gout.numel() + (3 if down is None else 4) * inp.numel())
+    with _timed("tshift_bwd", 0, nb, inp, ("GBND " if down is not None else "GBN ") + _shp(inp)):
         rc = lib.sgcn_tshift_bwd_gbn(_ptr(gout), _ptr(inp), _ptr(xpos), _ptr(ypos),
                                      _ptr(st.scale), _ptr(st.shift), _ptr(st.mean),
                                      _ptr(st.invstd), _ptr(bpart), _ptr(z), _ptr(zst.mean),
-                                     _ptr(zst.invstd), _ptr(zpart), _ptr(gin), _ptr(gx),
-                                     _ptr(gy), _ptr(ws), nbytes, B, C, H, W, _stream(inp))
+                                     _ptr(zst.invstd), _ptr(zpart), _ptr(d),
+                                     _ptr(dst.mean if dst is not None else None),
+                                     _ptr(dst.invstd if dst is not None else None),
+                                     _ptr(dpart), _ptr(gin), _ptr(gx), _ptr(gy), _ptr(ws),
+                                     nbytes, B, C, H, W, _stream(inp))
     _lib.check(rc, "sgcn_tshift_bwd_gbn")
+    if down is not None:
+        return gin, (pp if pp is not None else gx), gy, bpart, zpart, dpart
     return gin, (pp if pp is not None else gx), gy, bpart, zpart
 
 

@@ -114,8 +114,8 @@ def test_unit_parity_with_gbn_off(monkeypatch):
 
 
 def test_gbn_path_taken_in_model(monkeypatch):
-    """Units without a down conv take the fused path: no bn_bwd_reduce on their per-joint
-    BatchNorm (only l1/l5/l8, which have down convs, and the unit-tail reduces remain)."""
+    """Every unit takes the fused path (l1 / l5 / l8 with their down BatchNorm's sums too):
+    no bn_bwd_reduce on a per-joint BatchNorm remains (only the unit-tail reduces)."""
     import shiftgcn
     from shiftgcn import ops
     calls = {"gbn": 0, "pj_reduce": 0}
@@ -135,4 +135,45 @@ def test_gbn_path_taken_in_model(monkeypatch):
                        graph="graph.ntu_rgb_d.Graph").to(DEV).train()
     m(torch.randn(2, 3, 16, 25, 2, device=DEV)).sum().backward()
     torch.cuda.synchronize()
-    assert calls == {"gbn": 7, "pj_reduce": 3}, calls
+    assert calls == {"gbn": 10, "pj_reduce": 0}, calls
+
+
+@pytest.mark.parametrize("case", [(4, 64, 30, 25), (2, 16, 300, 25), (3, 32, 9, 33),
+                                  (2, 16, 40, 25, "wide")],
+                         ids=["4x64x30x25", "2x16x300x25", "3x32x9x33", "wide"])
+def test_gbn_down_sums_match_two_pass(case):
+    """With a down conv (H = relu(bn(Z) + bnd(D))), the down BatchNorm's backward sums from
+    the same launch (sgcn_tshift_bwd_gbn d_part, finalized with V = 1) match the two-pass
+    form (sgcn_bn_bwd_reduce with the residual BatchNorm + sgcn_bn_bwd_finalize) and fp64;
+    the gcn BatchNorm's sums are unchanged by the extra operand."""
+    from shiftgcn import ops
+    B, C, T, V = case[:4]
+    Z, H, dAs, xpos, ypos, bn_t, bn_g, ast, zst = _setup(B, C, T, V, 3 + sum(case[:4]),
+                                                         wide=len(case) > 4)
+    g = torch.Generator().manual_seed(11)
+    D = (torch.randn(B, C, T, V, generator=g) * 1.5 - 0.2).to(DEV)
+    bn_d = nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn_d.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn_d.bias.copy_(torch.randn(C, generator=g))
+    dst = ops.bn_finalize(ops.moments(D, False), B, C, T * V, bn_d)
+    dA1, gx1, gy1, part1, z6 = ops.tshift_bwd_gbn(dAs, H, xpos, ypos, ast, Z, zst)
+    dA2, gx2, gy2, part2, z6d, d6 = ops.tshift_bwd_gbn(dAs, H, xpos, ypos, ast, Z, zst,
+                                                        down=(D, dst))
+    torch.cuda.synchronize()
+    assert torch.equal(dA1, dA2) and torch.equal(part1, part2) and torch.equal(z6, z6d)
+    coefA, _, _ = ops.bn_bwd_finalize(part1, B, C, B * T * V, ast, bn_t)
+    rp, rpart = ops.bn_bwd_reduce(dA1, H, True, Z, zst, 3, r=D, rst=dst, dy_coef=coefA)
+    c_ref, dg_ref, db_ref = ops.bn_bwd_finalize(rpart, B, C, B * T * V, dst, bn_d)
+    c_new, dg_new, db_new = ops.bn_bwd_finalize_gbn(d6, B, C, 1, B * T * V, coefA, ast, dst,
+                                                    bn_d)
+    k = coefA.double()
+    gd = (k[0].view(1, C, 1, 1) * dA1.double() + k[1].view(1, C, 1, 1) * H.double()
+          + k[2].view(1, C, 1, 1)) * (H > 0)
+    dh = (D.double() - dst.mean.double().view(1, C, 1, 1)) * dst.invstd.double().view(1, C, 1, 1)
+    torch.cuda.synchronize()
+    assert _rel(db_new, gd.sum((0, 2, 3))) < 1e-5
+    assert _rel(dg_new, (gd * dh).sum((0, 2, 3))) < 1e-5
+    assert _rel(db_new, db_ref) < 1e-5 and _rel(dg_new, dg_ref) < 1e-5
+    assert _rel(c_new[0], c_ref[0]) == 0.0
+    assert _rel(c_new[1], c_ref[1]) < 1e-5 and _rel(c_new[2], c_ref[2]) < 1e-5
