@@ -28,7 +28,7 @@ extern "C" {
  * variants are gone (the S-free unit tail's statistics-only shift and re-formed bn2 input,
  * the re-forming temporal-shift weight gradient, per_joint = 1 / 2 rotated-store layouts).
  * 20: sgcn_tshift_bwd_gbn also takes the down conv's BatchNorm (d, d_mean, d_invstd,
- * d_part; NULL when the Shift_gcn has none). */
+ * d_part; NULL when the Shift_gcn has none); sgcn_sgd_step (the optimizer update). */
 int sgcn_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
@@ -387,6 +387,23 @@ int sgcn_pool(const float* x, float* out, int N, int M, int C, long long P, void
  * 16-byte aligned. */
 int sgcn_pool_bwd(const float* dout, float* dx, int N, int M, int C, long long P,
                   void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Optimizer (main.py:301-322, 414: torch.optim.SGD, dampening 0, not maximize)
+ * ------------------------------------------------------------------------------------ */
+
+/* Elements per chunk of the sgcn_sgd_step chunk map. */
+int sgcn_sgd_chunk_elems(void);
+
+/* One SGD step of every parameter tensor in ONE launch. `table` (device) holds per tensor
+ * five int64 {param, grad, momentum buffer (fp32 device pointers), (float weight_decay bits)
+ * | (float lr bits) << 32, flags (bit 0: the momentum buffer is new: initialised to the
+ * step's d_p, torch's clone)}; `numel` (device int32) per tensor; `chunks` (device int32)
+ * {tensor, first element} per chunk of at most sgcn_sgd_chunk_elems() elements. Per
+ * element, torch's order: d = g + wd*p (wd != 0); b = first ? d : momentum*b + d (momentum
+ * != 0); d = nesterov ? d + momentum*b : b; p = p - lr*d. */
+int sgcn_sgd_step(const void* table, const int* numel, const int* chunks, int n_chunks,
+                  float momentum, int nesterov, void* stream);
 
 #ifdef __cplusplus
 }  /* extern "C" */

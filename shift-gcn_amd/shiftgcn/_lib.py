@@ -31,6 +31,8 @@ _L = ctypes.c_longlong
 # name -> (restype, argtypes); mirrors include/shiftgcn.h
 SIGNATURES = {
     "sgcn_abi_version": (_I, []),
+    "sgcn_sgd_chunk_elems": (_I, []),
+    "sgcn_sgd_step": (_I, [_P, _P, _P, _I, _F, _I, _P]),
     "sgcn_tshift_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "sgcn_tshift_fwd_pre": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
                                  _I, _I, _P]),

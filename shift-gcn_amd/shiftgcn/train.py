@@ -38,10 +38,93 @@ def merged_param_groups(model: torch.nn.Module, base_lr: float):
     return [{"params": ps, "lr": base_lr, "weight_decay": wd} for wd, ps in by_wd.items()]
 
 
-def build_optimizer(model, base_lr=0.1, nesterov=True, momentum=0.9, merge_groups=True):
+class FusedSGD(torch.optim.SGD):
+    """``torch.optim.SGD`` (same constructor, param groups, hyper-parameters and state:
+    ``state[p]["momentum_buffer"]``, so ``state_dict`` / ``load_state_dict`` round-trip with
+    the stock optimizer) whose ``step`` updates every parameter of every group in ONE
+    launch (``sgcn_sgd_step``) instead of torch's ~35 multi-tensor launches per step.
+    Same arithmetic in the same order as torch's single/multi-tensor SGD (weight decay,
+    momentum with the first-step clone, nesterov, update); groups must share momentum,
+    dampening 0, nesterov and not maximize — otherwise, and for CPU or non-fp32
+    parameters, the stock ``step`` runs. Closures are supported as in torch."""
+
+    def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                 nesterov=False, **kw):
+        kw.pop("foreach", None)
+        super().__init__(params, lr=lr, momentum=momentum, dampening=dampening,
+                         weight_decay=weight_decay, nesterov=nesterov, foreach=True, **kw)
+        self._layout = None   # (param signature, device numel / chunk map, n chunks)
+
+    def _native_ok(self, items):
+        g0 = self.param_groups[0]
+        for g in self.param_groups:
+            if (g["momentum"] != g0["momentum"] or g["nesterov"] != g0["nesterov"] or
+                    g["dampening"] != 0 or g.get("maximize", False) or
+                    g.get("differentiable", False)):
+                return False
+        return all(p.is_cuda and p.dtype == torch.float32 and p.grad.dtype == torch.float32
+                   and not p.grad.is_sparse and p.is_contiguous() and p.grad.is_contiguous()
+                   for p, _ in items) and len({p.device for p, _ in items}) == 1
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        items = [(p, g) for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if not items:
+            return loss
+        if not self._native_ok(items):
+            return super().step()
+        import struct
+
+        from . import _lib
+        from .ops import _stream
+        lib = _lib.load()
+        g0 = self.param_groups[0]
+        momentum = float(g0["momentum"])
+        dev = items[0][0].device
+        sig = tuple((id(p), p.numel()) for p, _ in items)
+        if self._layout is None or self._layout[0] != sig:
+            ch = lib.sgcn_sgd_chunk_elems()
+            numel = [p.numel() for p, _ in items]
+            chunks = [v for t, n in enumerate(numel) for s0 in range(0, n, ch) for v in (t, s0)]
+            self._layout = (sig, torch.tensor(numel, dtype=torch.int32, device=dev),
+                            torch.tensor(chunks, dtype=torch.int32, device=dev),
+                            len(chunks) // 2)
+        _, numel_d, chunks_d, nchunks = self._layout
+        rows = []
+        for g in self.param_groups:
+            wdlr = struct.unpack("<q", struct.pack("<ff", float(g["weight_decay"]),
+                                                  float(g["lr"])))[0]
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                first = 0
+                if momentum != 0 and st.get("momentum_buffer") is None:
+                    st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.preserve_format)
+                    first = 1
+                buf = st.get("momentum_buffer") if momentum != 0 else p
+                rows += [p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), wdlr, first]
+        table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+        rc = lib.sgcn_sgd_step(table.data_ptr(), numel_d.data_ptr(), chunks_d.data_ptr(),
+                               nchunks, momentum, int(bool(g0["nesterov"])), _stream(table))
+        _lib.check(rc, "sgcn_sgd_step")
+        return loss
+
+
+def build_optimizer(model, base_lr=0.1, nesterov=True, momentum=0.9, merge_groups=True,
+                    fused=None):
+    """The reference's SGD; ``fused``: the one-launch native update (:class:`FusedSGD`;
+    default on, ``SGCN_FUSED_SGD=0`` selects torch's foreach SGD for A/B runs)."""
+    if fused is None:
+        import os
+        fused = os.environ.get("SGCN_FUSED_SGD", "1") != "0"
     groups = (merged_param_groups if merge_groups else sgd_param_groups)(model, base_lr)
-    return torch.optim.SGD(groups, lr=base_lr, momentum=momentum, nesterov=nesterov,
-                           foreach=True)
+    cls = FusedSGD if fused else torch.optim.SGD
+    return cls(groups, lr=base_lr, momentum=momentum, nesterov=nesterov, foreach=True)
 
 
 def adjust_learning_rate(optimizer, epoch, base_lr=0.1, steps=(60, 80, 100), warm_up_epoch=0):
