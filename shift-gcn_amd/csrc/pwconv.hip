@@ -77,11 +77,17 @@ struct FwdArgs {
 // nothing else reads. Compiled out of the product library.
 #ifdef SGCN_PW_STAMPS
 __device__ unsigned long long* g_pw_stamps;
+__device__ unsigned long long* g_pw_where;
 #define SGCN_PW_STAMP(i)                                                                  \
   do {                                                                                    \
-    if (threadIdx.x == 0)                                                                 \
-      g_pw_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (i)] =              \
-          __builtin_amdgcn_s_memtime();                                                   \
+    if (threadIdx.x == 0) {                                                               \
+      const size_t wgi = (size_t)blockIdx.y * gridDim.x + blockIdx.x;                     \
+      g_pw_stamps[wgi * 4 + (i)] = __builtin_amdgcn_s_memtime();                          \
+      /* where the workgroup runs: HW_ID (CU / SH / SE) and XCC_ID */                     \
+      if ((i) == 0 && g_pw_where)                                                         \
+        g_pw_where[wgi] = ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32) |  \
+                          (unsigned)__builtin_amdgcn_s_getreg(63492);                     \
+    }                                                                                     \
   } while (0)
 #else
 #define SGCN_PW_STAMP(i) do {} while (0)

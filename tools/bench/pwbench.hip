@@ -92,9 +92,11 @@ int main(int argc, char** argv) {
     {"l9 tcn 256 T75", 128, 256, 256, 75, 25, false, false},
     {"l9 gcn 256 T75", 128, 256, 256, 75, 25, true, true},
     {"l5 tcn 128 T300", 128, 128, 128, 300, 25, false, false},
+    {"l8 tcn-in 256x128 T150", 128, 256, 128, 150, 25, false, false},
+    {"l5 gcn 128x64 T300", 128, 128, 64, 300, 25, true, true},
   };
   hipStream_t st; CK(hipStreamCreate(&st));
-  size_t maxe = (size_t)128 * 128 * 300 * 25;
+  size_t maxe = (size_t)128 * 256 * 150 * 25;
   float *x, *y, *y2, *y3, *w, *mask, *ws, *dw1, *dw2;
   CK(hipMalloc(&x, maxe * 4)); CK(hipMalloc(&y, maxe * 4)); CK(hipMalloc(&y2, maxe * 4)); CK(hipMalloc(&y3, maxe * 4));
   CK(hipMalloc(&w, 256 * 256 * 4)); CK(hipMalloc(&mask, 64 * 256 * 4));
@@ -121,8 +123,18 @@ int main(int argc, char** argv) {
                     y2, s.M * N, N, 1, s.rot ? 1 : 0, 0, 0, s.B, s.M, s.K, s.T, s.V, st);
       };
       float us = timeit(L, st, 20);
-      printf("%-20s %-26s %8.1f us  %6.1f TF/s  %6.2f TB/s\n", s.name, "fwd product", us,
-             fl / us / 1e6, by / us / 1e6);
+      // bit hash of the output, to compare builds (e.g. -DSGCN_PW_RPT=n) with each other
+      const size_t ny = (size_t)s.B * s.M * N;
+      g_h1.resize(ny);
+      CK(hipMemcpy(g_h1.data(), y2, ny * 4, hipMemcpyDeviceToHost));
+      unsigned long long hsh = 1469598103934665603ull;
+      for (size_t i = 0; i < ny; ++i) {
+        unsigned u;
+        memcpy(&u, &g_h1[i], 4);
+        hsh = (hsh ^ u) * 1099511628211ull;
+      }
+      printf("%-20s %-26s %8.1f us  %6.1f TF/s  %6.2f TB/s  hash %016llx\n", s.name,
+             "fwd product", us, fl / us / 1e6, by / us / 1e6, hsh);
       if (argc > 2) {
         FwdArgs v = a;
         v.y.ptr = y3;

@@ -19,7 +19,7 @@ static double med(std::vector<double> v) {
   return v.empty() ? 0 : v[v.size() / 2];
 }
 
-int main() {
+int main(int argc, char** argv) {
   Shape shapes[] = {
     {"l2 tcn 64x64 T300", 128, 64, 64, 300, 25, 0},
     {"l2 gcn 64x64 T300 rot", 128, 64, 64, 300, 25, 1},
@@ -43,6 +43,11 @@ int main() {
   const size_t maxwg = 1 << 20;
   CK(hipMalloc(&stamps, maxwg * 4 * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(sgcn::g_pw_stamps), &stamps, sizeof(stamps)));
+  unsigned long long* where;
+  CK(hipMalloc(&where, maxwg * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(sgcn::g_pw_where), &where, sizeof(where)));
+  const char* dump = argc > 1 ? argv[1] : nullptr;   // per-workgroup CSV prefix
+  int si = 0;
   for (auto& s : shapes) {
     const long long N = (long long)s.T * s.V;
     auto L = [&]() {
@@ -73,6 +78,21 @@ int main() {
       t0 = std::min(t0, q[0]);
       t1 = std::max(t1, q[3]);
     }
+    if (dump) {
+      std::vector<unsigned long long> hw((size_t)nwg);
+      CK(hipMemcpy(hw.data(), where, hw.size() * 8, hipMemcpyDeviceToHost));
+      char fn[512];
+      snprintf(fn, sizeof fn, "%s_%d.csv", dump, si);
+      FILE* f = fopen(fn, "w");
+      fprintf(f, "wg,t0,t1,t2,t3,xcc,hwid\n");
+      for (int i = 0; i < nwg; ++i) {
+        const unsigned long long* q = &h[(size_t)i * 4];
+        fprintf(f, "%d,%llu,%llu,%llu,%llu,%llu,%llu\n", i, q[0] - t0, q[1] - t0, q[2] - t0,
+                q[3] - t0, hw[i] >> 32, hw[i] & 0xffffffffull);
+      }
+      fclose(f);
+    }
+    ++si;
     printf("%-24s %7.1f us  wg=%6d  median cycles: prologue %7.0f  main %7.0f  epilogue %7.0f"
            "  total %7.0f  (span %.0f cyc)\n", s.name, ms * 1e3, nwg, med(pro), med(mainl),
            med(epi), med(tot), (double)(t1 - t0));
