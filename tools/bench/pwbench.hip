@@ -94,6 +94,9 @@ int main(int argc, char** argv) {
     {"l5 tcn 128 T300", 128, 128, 128, 300, 25, false, false},
     {"l8 tcn-in 256x128 T150", 128, 256, 128, 150, 25, false, false},
     {"l5 gcn 128x64 T300", 128, 128, 64, 300, 25, true, true},
+    {"l1 gcn 64x3 T300", 128, 64, 3, 300, 25, false, false},
+    {"l1 dX 3x64 T300", 128, 3, 64, 300, 25, false, false},
+    {"l5 dX 64x128 T300", 128, 64, 128, 300, 25, false, false},
   };
   hipStream_t st; CK(hipStreamCreate(&st));
   size_t maxe = (size_t)128 * 256 * 150 * 25;
