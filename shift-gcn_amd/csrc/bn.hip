@@ -162,12 +162,14 @@ __global__ __launch_bounds__(NT) void moments_ja_kernel(const float* __restrict_
   }
 }
 
-// Per-feature sums over the batch of float2 partials: ONE WAVE PER FEATURE, the lanes
-// striding the batch (4 partials in flight per lane: one round trip for B <= 256), then a
-// fixed xor tree over the wave in double (deterministic). These kernels are pure latency
-// (a few MB of partials); a wave-level tree replaces the former LDS slice merge (32
-// dependent LDS reads). Every lane returns the three double sums (x, y, x*x).
-constexpr int kFW = 4;   // features (waves) per 256-thread block
+// Per-feature sums over the batch of float2 partials part[b][f]: a workgroup takes 64
+// consecutive features (the lanes: each load reads 512 contiguous bytes) and its kFSW waves
+// take every kFSW-th sample, 4 rows in flight, then a fixed-order merge through LDS in
+// double (deterministic). Lane l of wave 0 returns feature blockIdx.x*64 + l's three double
+// sums (x, y, x*x). (One wave per feature with the lanes striding the batch cost a cache
+// line per lane and load.)
+constexpr int kFW = 4;    // features (waves) per 256-thread block (mask_grad_finalize)
+constexpr int kFSW = 8;   // waves per 64 features in the BatchNorm finalizes
 __device__ __forceinline__ double wave_dsum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
@@ -175,17 +177,16 @@ __device__ __forceinline__ double wave_dsum(double v) {
 }
 __device__ __forceinline__ bool feature_sums(const float2* __restrict__ part, int B, int F,
                                              double& sx, double& sy, double& sxx, int& f) {
-  const int lane = threadIdx.x & 63;
-  f = blockIdx.x * kFW + (int)(threadIdx.x >> 6);
+  __shared__ double red[kFSW - 1][3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  f = blockIdx.x * 64 + lane;
   const int fc = min(f, F - 1);
   double ax = 0.0, ay = 0.0, axx = 0.0;
-  for (int b0 = lane; b0 < B; b0 += 64 * 4) {
+  int b = w;
+  for (; b + 3 * kFSW < B; b += 4 * kFSW) {
     float2 pv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int b = b0 + u * 64;
-      pv[u] = b < B ? part[(size_t)b * F + fc] : make_float2(0.f, 0.f);
-    }
+    for (int u = 0; u < 4; ++u) pv[u] = part[(size_t)(b + u * kFSW) * F + fc];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       ax += pv[u].x;
@@ -193,15 +194,33 @@ __device__ __forceinline__ bool feature_sums(const float2* __restrict__ part, in
       axx += (double)pv[u].x * pv[u].x;
     }
   }
-  sx = wave_dsum(ax);
-  sy = wave_dsum(ay);
-  sxx = wave_dsum(axx);
-  return f < F && lane == 0;
+  for (; b < B; b += kFSW) {
+    const float2 pv = part[(size_t)b * F + fc];
+    ax += pv.x;
+    ay += pv.y;
+    axx += (double)pv.x * pv.x;
+  }
+  if (w) {
+    red[w - 1][0][lane] = ax;
+    red[w - 1][1][lane] = ay;
+    red[w - 1][2][lane] = axx;
+  }
+  __syncthreads();
+  if (w) return false;
+  for (int q = 0; q < kFSW - 1; ++q) {
+    ax += red[q][0][lane];
+    ay += red[q][1][lane];
+    axx += red[q][2][lane];
+  }
+  sx = ax;
+  sy = ay;
+  sxx = axx;
+  return f < F;
 }
 
 // part layout [B][F] of {mean, M2}, each over n_part elements. Equal counts, so
 // mean = avg(mean_b), M2 = sum M2_b + n_part * sum (mean_b - mean)^2 (double).
-__global__ __launch_bounds__(64 * kFW) void bn_finalize_kernel(
+__global__ __launch_bounds__(64 * kFSW) void bn_finalize_kernel(
     const float2* __restrict__ part, int B, int F, int n_part, int perm_V,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
@@ -614,7 +633,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_ja_kernel(
 
 // dgamma = sum g*xhat, dbeta = sum g; dx = k1*g + k2*x + k3 with
 // k1 = gamma*invstd, k2 = -k1*invstd*mean(g*xhat), k3 = -k1*mean(g) - k2*mean_x
-__global__ __launch_bounds__(64 * kFW) void bn_bwd_finalize_kernel(
+__global__ __launch_bounds__(64 * kFSW) void bn_bwd_finalize_kernel(
     const float2* __restrict__ part, int B, int F, double n_total, int perm_V,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
@@ -641,34 +660,49 @@ __global__ __launch_bounds__(64 * kFW) void bn_bwd_finalize_kernel(
 //   part6[j][b][f], j = {sum dA, sum (H-mu), sum 1, sum dA*zh, sum (H-mu)*zh, sum zh}
 // over the active (H > 0) positions, g = k1*dA + k2*(H - mu) + (k3 + k2*mu) with
 // k = dyc[3][C] (Shift_tcn.bn's backward coefficients) and mu = dym[C] (its batch mean),
-// channel c = f / V. The six sums are merged over b in double (32 features x 16 slices,
-// fixed order), then combined once per feature.
-__global__ __launch_bounds__(64 * kFW) void bn_bwd_finalize_gbn_kernel(
+// channel c = f / V. The six sums are merged over b in double: a workgroup takes 64
+// consecutive features (the lanes: every load reads 256 contiguous bytes) and its
+// kGbnW waves take every kGbnW-th sample (4 rows in flight), merged in fixed order
+// through LDS. (The one-wave-per-feature form with lanes striding the batch cost a cache
+// line per lane and load: 19 us average per call at F = 1,600-6,400, B = 128.)
+constexpr int kGbnW = 16;
+__global__ __launch_bounds__(64 * kGbnW) void bn_bwd_finalize_gbn_kernel(
     const float* __restrict__ part6, int B, int F, int V, double n_total,
     const float* __restrict__ dyc, const float* __restrict__ dym, int C,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
     int accumulate, int batch_stats, float* __restrict__ coef) {
-  const int lane = threadIdx.x & 63;
-  const int f = blockIdx.x * kFW + (int)(threadIdx.x >> 6);
+  __shared__ double red[kGbnW - 1][6][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + lane;
   const int fc = min(f, F - 1);
   const size_t np = (size_t)B * F;
   double s6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int b0 = lane; b0 < B; b0 += 64 * 2) {
-    float pv[6][2];
+  int b = w;
+  for (; b + 3 * kGbnW < B; b += 4 * kGbnW) {
+    float pv[6][4];
 #pragma unroll
     for (int j = 0; j < 6; ++j)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int b = b0 + u * 64;
-        pv[j][u] = b < B ? part6[j * np + (size_t)b * F + fc] : 0.f;
-      }
+      for (int u = 0; u < 4; ++u) pv[j][u] = part6[j * np + (size_t)(b + u * kGbnW) * F + fc];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) s6[j] += (double)pv[j][0] + (double)pv[j][1];
+    for (int j = 0; j < 6; ++j)
+      s6[j] += ((double)pv[j][0] + (double)pv[j][1]) + ((double)pv[j][2] + (double)pv[j][3]);
   }
+  for (; b < B; b += kGbnW) {
 #pragma unroll
-  for (int j = 0; j < 6; ++j) s6[j] = wave_dsum(s6[j]);
-  if (f >= F || lane != 0) return;
+    for (int j = 0; j < 6; ++j) s6[j] += (double)part6[j * np + (size_t)b * F + fc];
+  }
+  if (w) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) red[w - 1][j][lane] = s6[j];
+  }
+  __syncthreads();
+  if (w || f >= F) return;
+  for (int q = 0; q < kGbnW - 1; ++q) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s6[j] += red[q][j][lane];
+  }
   const int c = f / V;
   const double k1 = dyc[c], k2 = dyc[C + c], c3 = (double)dyc[2 * C + c] + k2 * (double)dym[c];
   const double sg = k1 * s6[0] + k2 * s6[1] + c3 * s6[2];
@@ -1141,7 +1175,7 @@ int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
   SGCN_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
   hipStream_t st = (hipStream_t)stream;
-  bn_finalize_kernel<<<(F + kFW - 1) / kFW, 64 * kFW, 0, st>>>(
+  bn_finalize_kernel<<<(F + 63) / 64, 64 * kFSW, 0, st>>>(
       (const float2*)part, B, F, n_part, perm_V, gamma, beta, eps, momentum, running_mean,
       running_var, num_batches, mean, invstd, scale, shift);
   SGCN_LAUNCH_CHECK();
@@ -1320,7 +1354,7 @@ int sgcn_bn_bwd_finalize(const float* part, int B, int F, long long n_total, int
                          float* coef, void* stream) {
   SGCN_REQUIRE(part && B > 0 && F > 0 && n_total > 0 && mean && invstd && coef);
   SGCN_REQUIRE(perm_V <= 0 || F % perm_V == 0);
-  bn_bwd_finalize_kernel<<<(F + kFW - 1) / kFW, 64 * kFW, 0, (hipStream_t)stream>>>(
+  bn_bwd_finalize_kernel<<<(F + 63) / 64, 64 * kFSW, 0, (hipStream_t)stream>>>(
       (const float2*)part, B, F, (double)n_total, perm_V, mean, invstd, gamma, dgamma, dbeta,
       accumulate, batch_stats, coef);
   SGCN_LAUNCH_CHECK();
@@ -1335,7 +1369,7 @@ int sgcn_bn_bwd_finalize_gbn(const float* part6, int B, int C, int V, long long 
   SGCN_REQUIRE(part6 && B > 0 && C > 0 && V > 0 && n_total > 0 && dy_coef && dy_mean && mean &&
                invstd && coef);
   const int F = C * V;
-  bn_bwd_finalize_gbn_kernel<<<(F + kFW - 1) / kFW, 64 * kFW, 0, (hipStream_t)stream>>>(
+  bn_bwd_finalize_gbn_kernel<<<(F + 63) / 64, 64 * kGbnW, 0, (hipStream_t)stream>>>(
       part6, B, F, V, (double)n_total, dy_coef, dy_mean, C, mean, invstd, gamma, dgamma, dbeta,
       accumulate, batch_stats, coef);
   SGCN_LAUNCH_CHECK();

@@ -1,5 +1,5 @@
 """Per-step view of a rocprofv3 kernel trace (kernel_trace.csv) of bench.py: for every
-training step (delimited by the optimizer's first multi-tensor kernel) the wall time, the
+training step (delimited by the optimizer's launch) the wall time, the
 busy time (union of kernel intervals), the summed kernel time per hardware queue (the
 side-stream weight gradients run on their own queue), and, for the last step that used
 more than one queue, the per-kernel-class sums.
@@ -37,7 +37,11 @@ def main():
     for p in sys.argv[1:]:
         rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                         r["Queue_Id"]) for r in csv.DictReader(open(p))), key=lambda r: r[1])
-        marks = [i for i, r in enumerate(rows) if "multi_tensor_apply" in r[0]]
+        # the optimizer's launch ends a step (FusedSGD: sgd_step_kernel; torch's SGD: its
+        # first multi-tensor kernel)
+        marks = [i for i, r in enumerate(rows) if "sgd_step_kernel" in r[0]]
+        if not marks:
+            marks = [i for i, r in enumerate(rows) if "multi_tensor_apply" in r[0]]
         starts = [marks[0]] + [m for a, m in zip(marks, marks[1:]) if m - a > 5]
         print(p)
         last_multi = None
