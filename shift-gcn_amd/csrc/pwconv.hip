@@ -857,6 +857,87 @@ void launch_slab_reduce(const float* slab, const float* bslab, int S, int M, int
       slab, bslab, S, n, nb, M, Nc, dw, dbias, transpose, accum, baccum);
 }
 
+
+// ------------------------------------------------------------------------------------
+// dW for Nc <= 4 input channels (l1's gcn Linear and down conv, 3 -> 64): HBM-bound on G
+// (M rows), so no MFMA tile (which would stage 64 operand rows for 3 and multiply zeros):
+// each wave owns 16 rows of G, its 64 lanes walk 64 consecutive positions per step
+// (256-B row reads), the Nc X values of a position are shared by the wave's 16 rows, and
+// the per-lane sums are merged over the wave in a fixed xor order into slab[split]. Same
+// slab layout and reduction as pw_dw_kernel.
+// ------------------------------------------------------------------------------------
+constexpr int kDwcRows = 16;   // G rows per wave
+constexpr int kDwcMaxC = 4;
+template <int NC, bool MASK>
+__global__ __launch_bounds__(256) void pw_dw_smallc_kernel(DwArgs p, int pos_per_split) {
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m0 = (blockIdx.x * 4 + wid) * kDwcRows;   // this wave's first row
+  const int split = blockIdx.y;
+  const int V = p.V, N = p.T * V;
+  const long long P = (long long)p.B * N;
+  const long long q0 = (long long)split * pos_per_split;
+  const long long q1 = min(q0 + pos_per_split, P);
+  float acc[kDwcRows][NC], bs[kDwcRows];
+#pragma unroll
+  for (int r = 0; r < kDwcRows; ++r) {
+    bs[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[r][c] = 0.f;
+  }
+  if (m0 < p.M) {
+    for (long long q = q0 + lane; q < q1; q += 64) {
+      const int b = (int)(q / N);
+      const int n = (int)(q - (long long)b * N);
+      const int t = n / V, v = n - t * V;
+      const float* __restrict__ gb =
+          p.g.ptr + (long long)b * p.g.bstride + (long long)t * p.g.tstride * V;
+      const float* __restrict__ xb =
+          p.x.ptr + (long long)b * p.x.bstride + (long long)t * p.x.tstride * V;
+      float xv[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int cc = min(c, p.Nc - 1);
+        xv[c] = xb[cc * p.x.cstride + pmod(v + p.x.rsign * cc, V)];
+        if (MASK) xv[c] *= p.mask[v * p.Nc + cc];
+        if (c >= p.Nc) xv[c] = 0.f;
+      }
+      int cg = pmod(v + p.g.rsign * m0, V);
+      const int gstep = p.g.rsign < 0 ? V - 1 : (p.g.rsign > 0 ? 1 : 0);
+#pragma unroll
+      for (int r = 0; r < kDwcRows; ++r) {
+        const int m = min(m0 + r, p.M - 1);
+        const float gv = m0 + r < p.M ? gb[(long long)m * p.g.cstride + cg] : 0.f;
+        cg += gstep;
+        cg = cg >= V ? cg - V : cg;
+        bs[r] += gv;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[r][c] = fmaf(gv, xv[c], acc[r][c]);
+      }
+    }
+  }
+  // fixed-order wave merge; lane 0 writes the split's partials
+#pragma unroll
+  for (int r = 0; r < kDwcRows; ++r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      bs[r] += __shfl_xor(bs[r], o, 64);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[r][c] += __shfl_xor(acc[r][c], o, 64);
+    }
+  }
+  if (lane == 0 && m0 < p.M) {
+    float* slab = p.slab + (size_t)split * p.M * p.Nc;
+#pragma unroll
+    for (int r = 0; r < kDwcRows; ++r) {
+      if (m0 + r >= p.M) break;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < p.Nc) slab[(size_t)(m0 + r) * p.Nc + c] = acc[r][c];
+      if (p.bslab) p.bslab[(size_t)split * p.M + m0 + r] = bs[r];
+    }
+  }
+}
 // ------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------
@@ -973,6 +1054,19 @@ int dw_splits(int M, int Nc, int B, int N, int tiles) {
 
 int dw_tile(int X) { return X > 64 ? 128 : 64; }
 
+// pw_dw_smallc_kernel: Nc <= 4; ~1,024 workgroups of 4 x 16 rows over position splits
+#ifndef SGCN_DWC
+#define SGCN_DWC 1
+#endif
+bool use_dwc(int Nc) { return SGCN_DWC && Nc <= kDwcMaxC; }
+int dwc_splits(int M, long long P) {
+  const int mg = (M + 4 * kDwcRows - 1) / (4 * kDwcRows);
+  long long S = (1024 + mg - 1) / mg;
+  const long long per = (P + S - 1) / S;
+  if (per < 256) S = (P + 255) / 256;   // at least four 64-position steps per split
+  return (int)(S < 1 ? 1 : S);
+}
+
 // pw_dw3 measured faster from 128x128 contractions up (tools/bench/pwbench: l5/l6 tcn,
 // l9 tcn/gcn), equal or slower on the 64-wide masked/rotated ones
 bool use_dw3(int M, int Nc) { return (long long)M * Nc >= 128 * 128; }
@@ -1088,6 +1182,8 @@ int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long l
 }
 
 size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V) {
+  if (use_dwc(Nc))
+    return (size_t)dwc_splits(M, (long long)B * T * V) * ((size_t)M * Nc + M) * sizeof(float);
   if (use_dw3(M, Nc)) return dw3_ws_bytes(B, M, Nc, T, V);
   const int tiles = ((M + dw_tile(M) - 1) / dw_tile(M)) * ((Nc + dw_tile(Nc) - 1) / dw_tile(Nc));
   const int S = dw_splits(M, Nc, B, T * V, tiles);
@@ -1115,7 +1211,21 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
   a.B = B;
   hipStream_t st = (hipStream_t)stream;
   int S;
-  if (use_dw3(M, Nc)) {
+  if (use_dwc(Nc)) {
+    const long long P = (long long)B * T * V;
+    S = dwc_splits(M, P);
+    a.slab = (float*)ws;
+    a.bslab = dbias ? (float*)ws + (size_t)S * M * Nc : nullptr;
+    const int per = (int)((P + S - 1) / S);
+    dim3 grid((M + 4 * kDwcRows - 1) / (4 * kDwcRows), S);
+#define SGCN_DWC_L(NC_) (mask ? pw_dw_smallc_kernel<NC_, true><<<grid, 256, 0, st>>>(a, per) \
+                              : pw_dw_smallc_kernel<NC_, false><<<grid, 256, 0, st>>>(a, per))
+    if (Nc == 1) SGCN_DWC_L(1);
+    else if (Nc == 2) SGCN_DWC_L(2);
+    else if (Nc == 3) SGCN_DWC_L(3);
+    else SGCN_DWC_L(4);
+#undef SGCN_DWC_L
+  } else if (use_dw3(M, Nc)) {
     a.g_bytes = plane_bytes(g_bstride, g_cstride, g_tstride, B, M, T, V);
     a.x_bytes = plane_bytes(x_bstride, x_cstride, x_tstride, B, Nc, T, V);
     a.mask_bytes = mask ? (unsigned)(V * Nc * 4) : 0u;

@@ -80,7 +80,7 @@ def test_pw_fwd_time_stride(M):
 
 
 @pytest.mark.parametrize("M,Nc", [(64, 3), (64, 64), (128, 64), (128, 128), (256, 256),
-                                  (64, 128), (37, 100)])
+                                  (64, 128), (37, 100), (64, 1), (100, 2), (17, 4)])
 @pytest.mark.parametrize("grot,xrot,mask,transpose", [(0, 0, False, False),
                                                        (1, 1, True, True)])
 def test_pw_dw_matches_torch(M, Nc, grot, xrot, mask, transpose):
