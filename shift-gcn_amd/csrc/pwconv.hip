@@ -938,6 +938,70 @@ __global__ __launch_bounds__(256) void pw_dw_smallc_kernel(DwArgs p, int pos_per
     }
   }
 }
+
+// ------------------------------------------------------------------------------------
+// Forward / dX contraction with M <= 4 output rows (l1's input gradients, 64 -> 3): one
+// position per lane, the K input rows read straight from HBM (coalesced over the lanes'
+// consecutive positions, 8 rows in flight), the M x K weights broadcast from LDS (one
+// 16-byte read per k). HBM-bound on the K-row operand; the 64-row MFMA tile would stage
+// and multiply 61 rows of zeros. Same bias / ReLU / accumulate epilogue as pwg_fwd_kernel.
+// ------------------------------------------------------------------------------------
+constexpr int kSmallM = 4;
+template <bool AMC, bool ACCUM>
+__global__ __launch_bounds__(256) void pw_fwd_smallm_kernel(FwdArgs p) {
+  __shared__ float4 Ws[256];   // [k] -> (m0..m3), zero past M
+  const int tid = threadIdx.x;
+  const int K = p.K, M = p.M, V = p.V, N = p.T * V;
+  for (int k = tid; k < K; k += 256) {
+    float w[kSmallM];
+#pragma unroll
+    for (int m = 0; m < kSmallM; ++m)
+      w[m] = m < M ? (AMC ? p.A[k * p.lda + m] : p.A[m * p.lda + k]) : 0.f;
+    Ws[k] = make_float4(w[0], w[1], w[2], w[3]);
+  }
+  __syncthreads();
+  const long long q = (long long)blockIdx.x * 256 + tid;
+  if (q >= (long long)p.B * N) return;
+  const int b = (int)(q / N);
+  const int n = (int)(q - (long long)b * N);
+  const int t = n / V, v = n - t * V;
+  const float* __restrict__ xp =
+      p.x.ptr + (long long)b * p.x.bstride + (long long)t * p.x.tstride * V + v;
+  float* __restrict__ yp = p.y.ptr + (long long)b * p.y.bstride + (long long)t * p.y.tstride * V + v;
+  const long long xcs = p.x.cstride;
+  float acc[kSmallM] = {0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= K; k += 8) {
+    float xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = xp[(k + u) * xcs];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float4 w = Ws[k + u];
+      acc[0] = fmaf(w.x, xv[u], acc[0]);
+      acc[1] = fmaf(w.y, xv[u], acc[1]);
+      acc[2] = fmaf(w.z, xv[u], acc[2]);
+      acc[3] = fmaf(w.w, xv[u], acc[3]);
+    }
+  }
+  for (; k < K; ++k) {
+    const float xv = xp[k * xcs];
+    const float4 w = Ws[k];
+    acc[0] = fmaf(w.x, xv, acc[0]);
+    acc[1] = fmaf(w.y, xv, acc[1]);
+    acc[2] = fmaf(w.z, xv, acc[2]);
+    acc[3] = fmaf(w.w, xv, acc[3]);
+  }
+#pragma unroll
+  for (int m = 0; m < kSmallM; ++m) {
+    if (m >= M) break;
+    float val = acc[m] + (p.bias ? p.bias[m] : 0.f);
+    if (p.relu) val = fmaxf(val, 0.f);
+    float* dst = yp + (long long)m * p.y.cstride;
+    if (ACCUM) val += *dst;
+    *dst = val;
+  }
+}
 // ------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------
@@ -1058,6 +1122,9 @@ int dw_tile(int X) { return X > 64 ? 128 : 64; }
 #ifndef SGCN_DWC
 #define SGCN_DWC 1
 #endif
+#ifndef SGCN_SMALLM
+#define SGCN_SMALLM 0   // pw_fwd_smallm_kernel: built, default off until measured on hardware
+#endif
 bool use_dwc(int Nc) { return SGCN_DWC && Nc <= kDwcMaxC; }
 int dwc_splits(int M, long long P) {
   const int mg = (M + 4 * kDwcRows - 1) / (4 * kDwcRows);
@@ -1126,7 +1193,16 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   // sharing that read with the `down` conv (verdict r02, row f2) could save
   if (x_tstride == 2 && !ac) a.x_bytes = 0;
 #endif
-  if (M <= 64) launch_pwg<64, 256, 2, 4>(a, ac, st);
+  if (M <= kSmallM && SGCN_SMALLM && !mask && x_rsign == 0 && y_rsign == 0) {
+    const unsigned grid = (unsigned)(((long long)B * T * V + 255) / 256);
+    if (w_mcontig) {
+      if (ac) pw_fwd_smallm_kernel<true, true><<<grid, 256, 0, st>>>(a);
+      else pw_fwd_smallm_kernel<true, false><<<grid, 256, 0, st>>>(a);
+    } else {
+      if (ac) pw_fwd_smallm_kernel<false, true><<<grid, 256, 0, st>>>(a);
+      else pw_fwd_smallm_kernel<false, false><<<grid, 256, 0, st>>>(a);
+    }
+  } else if (M <= 64) launch_pwg<64, 256, 2, 4>(a, ac, st);
   else if (M <= 128) launch_pwg<128, 256, 2, 4>(a, ac, st);
   else launch_pwg<256, 128, 4, 2>(a, ac, st);
   SGCN_LAUNCH_CHECK();

@@ -28,7 +28,8 @@ def rot_scatter(y, sign):
 
 
 @pytest.mark.parametrize("M,K", [(64, 3), (64, 64), (128, 64), (128, 128), (256, 128),
-                                 (256, 256), (3, 64), (64, 256), (100, 37), (37, 51), (17, 64)])
+                                 (256, 256), (3, 64), (64, 256), (100, 37), (37, 51), (17, 64),
+                                 (4, 130), (1, 7)])
 @pytest.mark.parametrize("rin,rout,mask", [(0, 0, False), (1, 1, True), (1, 0, False)])
 def test_pw_fwd_matches_torch(M, K, rin, rout, mask):
     from shiftgcn import ops
