@@ -1123,7 +1123,7 @@ int dw_tile(int X) { return X > 64 ? 128 : 64; }
 #define SGCN_DWC 1
 #endif
 #ifndef SGCN_SMALLM
-#define SGCN_SMALLM 0   // pw_fwd_smallm_kernel: built, default off until measured on hardware
+#define SGCN_SMALLM 1
 #endif
 bool use_dwc(int Nc) { return SGCN_DWC && Nc <= kDwcMaxC; }
 int dwc_splits(int M, long long P) {
