@@ -39,8 +39,8 @@ def short(n):
 # op class (ops.LaunchTimer name) -> (primary kernel prefixes, helper kernel prefixes). The
 # primary kernels count the C-ABI calls; every kernel of the class adds to its bytes.
 OP_CLASSES = {
-    "pw_fwd": (("pwg_fwd_kernel",), ("tshift_params_kernel",)),
-    "pw_dw": (("pw_dw_kernel", "pw_dw3_kernel"), ("slab_reduce_kernel",)),
+    "pw_fwd": (("pwg_fwd_kernel", "pw_fwd_smallm_kernel"), ("tshift_params_kernel",)),
+    "pw_dw": (("pw_dw_kernel", "pw_dw3_kernel", "pw_dw_smallc_kernel"), ("slab_reduce_kernel",)),
     "tshift_fwd": (("tshift_fwd_kernel", "tshift_fwd_lds_kernel", "tshift_fwd_pad_kernel",
                     "tshift_fwd_pre_kernel", "tshift_fwd_tail_kernel"), ()),
     "tshift_bwd": (("tshift_bwd_kernel", "tshift_bwd_ra_kernel", "tshift_bwd_s2_kernel"), ()),
