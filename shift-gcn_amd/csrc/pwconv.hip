@@ -866,7 +866,10 @@ void launch_slab_reduce(const float* slab, const float* bslab, int S, int M, int
 // the per-lane sums are merged over the wave in a fixed xor order into slab[split]. Same
 // slab layout and reduction as pw_dw_kernel.
 // ------------------------------------------------------------------------------------
-constexpr int kDwcRows = 16;   // G rows per wave
+#ifndef SGCN_DWC_ROWS
+#define SGCN_DWC_ROWS 16
+#endif
+constexpr int kDwcRows = SGCN_DWC_ROWS;   // G rows per wave
 constexpr int kDwcMaxC = 4;
 template <int NC, bool MASK>
 __global__ __launch_bounds__(256) void pw_dw_smallc_kernel(DwArgs p, int pos_per_split) {
