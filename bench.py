@@ -242,7 +242,13 @@ def main():
     if distributed:
         broadcast_parameters(model)
     opt = train.build_optimizer(model, base_lr=0.1)
-    sync = GradAllReduce(model) if distributed else None
+    # N>1: the gradients are written into the all-reduce bucket by the backward and the
+    # 1/world is applied inside the one-launch optimizer update: one all-reduce + one update
+    # launch between backward() and the next step (shiftgcn.dist.GradAllReduce)
+    sync = None
+    if distributed:
+        sync = GradAllReduce(model, defer_scale_to=opt if isinstance(opt, train.FusedSGD)
+                             else None)
     gen = torch.Generator().manual_seed(1000 + rank)
     x = torch.randn(args.batch, 3, T, V, M, generator=gen).to(dev)
     label = torch.randint(0, num_class, (args.batch,), generator=gen).to(dev)

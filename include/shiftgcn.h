@@ -22,13 +22,19 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 20
+#define SGCN_ABI_VERSION 21
+/* Set in sgcn_abi_version()'s value by a diagnostic build (SGCN_PW_DIAG, SGCN_PW_STAMPS,
+ * SGCN_DIAG_*: timing probes whose results are WRONG, `make diag` only); the Python loader
+ * refuses such a library. */
+#define SGCN_ABI_DIAG_FLAG 0x10000
 
 /* ABI version of the loaded library (== SGCN_ABI_VERSION). 19: the measured-and-rejected
  * variants are gone (the S-free unit tail's statistics-only shift and re-formed bn2 input,
  * the re-forming temporal-shift weight gradient, per_joint = 1 / 2 rotated-store layouts).
  * 20: sgcn_tshift_bwd_gbn also takes the down conv's BatchNorm (d, d_mean, d_invstd,
- * d_part; NULL when the Shift_gcn has none); sgcn_sgd_step (the optimizer update). */
+ * d_part; NULL when the Shift_gcn has none); sgcn_sgd_step (the optimizer update).
+ * 21: sgcn_sgd_step's per-tensor gradient scale (flags bit 1 + the float in bits 32-63: the
+ * data-parallel reduction's 1/world applied inside the update, written back to the grad). */
 int sgcn_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
@@ -398,10 +404,12 @@ int sgcn_sgd_chunk_elems(void);
 /* One SGD step of every parameter tensor in ONE launch. `table` (device) holds per tensor
  * five int64 {param, grad, momentum buffer (fp32 device pointers), (float weight_decay bits)
  * | (float lr bits) << 32, flags (bit 0: the momentum buffer is new: initialised to the
- * step's d_p, torch's clone)}; `numel` (device int32) per tensor; `chunks` (device int32)
+ * step's d_p, torch's clone; bit 1: scale the gradient by the float whose bits are flags
+ * bits 32-63 and store the scaled gradient back, i.e. GradAllReduce's deferred
+ * `grad *= 1/world`)}; `numel` (device int32) per tensor; `chunks` (device int32)
  * {tensor, first element} per chunk of at most sgcn_sgd_chunk_elems() elements. Per
- * element, torch's order: d = g + wd*p (wd != 0); b = first ? d : momentum*b + d (momentum
- * != 0); d = nesterov ? d + momentum*b : b; p = p - lr*d. */
+ * element, torch's order: g = g*s (bit 1); d = g + wd*p (wd != 0); b = first ? d :
+ * momentum*b + d (momentum != 0); d = nesterov ? d + momentum*b : b; p = p - lr*d. */
 int sgcn_sgd_step(const void* table, const int* numel, const int* chunks, int n_chunks,
                   float momentum, int nesterov, void* stream);
 

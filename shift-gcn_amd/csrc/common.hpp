@@ -5,6 +5,15 @@
 
 #include "../../include/shiftgcn.h"
 
+// Diagnostic builds (timing probes whose results are wrong; `make diag` only): any of
+// these macros marks the library, and sgcn_abi_version() then carries SGCN_ABI_DIAG_FLAG.
+#if defined(SGCN_PW_DIAG) || defined(SGCN_PW_STAMPS) || defined(SGCN_DIAG_X1B_BOUND) || \
+    defined(SGCN_DIAG_F2_BOUND)
+#define SGCN_DIAG_BUILD 1
+#else
+#define SGCN_DIAG_BUILD 0
+#endif
+
 #define SGCN_LAUNCH_CHECK()                                   \
   do {                                                        \
     hipError_t e__ = hipGetLastError();                       \
@@ -125,6 +134,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 }
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+// the same with a cache-policy operand (bit 1 = nt, bit 4 = sc1; 0 = default)
+template <int AUX>
+__device__ __forceinline__ float bload_pol(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX));
 }
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, unsigned voff,
                                        unsigned soff) {

@@ -10,8 +10,11 @@
 //
 // Per tensor t the caller passes (device table, rewritten every step because fresh
 // gradient tensors are allocated every backward): {param, grad, momentum buffer, bits of
-// (float weight_decay, float lr), flags (bit 0: the momentum buffer is new)} as int64, and
-// a chunk map {tensor, first element} per workgroup.
+// (float weight_decay, float lr), flags (bit 0: the momentum buffer is new; bit 1: scale
+// the gradient by the float in bits 32-63 first and store it back)} as int64, and a chunk
+// map {tensor, first element} per workgroup. The scale is the data-parallel reduction's
+// 1/world (shiftgcn/dist.py): the all-reduced SUM is scaled here instead of by a separate
+// pass between the all-reduce and the update.
 #include "common.hpp"
 
 namespace sgcn {
@@ -35,10 +38,17 @@ __global__ __launch_bounds__(kSgdThreads) void sgd_step_kernel(
   const float wd = __uint_as_float((unsigned)(e.wdlr & 0xffffffffLL));
   const float lr = __uint_as_float((unsigned)((unsigned long long)e.wdlr >> 32));
   const bool first = (e.flags & 1) != 0;
+  const bool scaled = (e.flags & 2) != 0;
+  const float gs = __uint_as_float((unsigned)((unsigned long long)e.flags >> 32));
+  float* __restrict__ gw = reinterpret_cast<float*>(e.g);
   const int end = min(numel[t], start + kSgdChunk);
   for (int i = start + (int)threadIdx.x; i < end; i += kSgdThreads) {
     const float pv = p[i];
     float d = g[i];
+    if (scaled) {                                      // the reduction's grad *= 1/world
+      d = d * gs;
+      gw[i] = d;
+    }
     if (wd != 0.f) d = d + wd * pv;                    // grad + weight_decay * param
     float b;
     if (momentum != 0.f) {

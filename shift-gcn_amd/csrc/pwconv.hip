@@ -99,6 +99,15 @@ __device__ unsigned long long* g_pw_where;
 #ifndef SGCN_PW_DIAG
 #define SGCN_PW_DIAG 0
 #endif
+// Cache policy of the forward contraction's plain X-operand loads and of its weight loads
+// (the aux operand of the buffer loads: 0 default, 2 nt, 16 sc1): tuning knobs
+// (tools/bench/ofetch), results unchanged.
+#ifndef SGCN_PW_XPOL
+#define SGCN_PW_XPOL 0
+#endif
+#ifndef SGCN_PW_APOL
+#define SGCN_PW_APOL 0
+#endif
 
 __device__ __forceinline__ int pmod(int a, int V) {
   int r = a % V;
@@ -284,7 +293,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         continue;
       }
       const unsigned voff = XROT ? xcol + (unsigned)(cv * 4) : xcol;
-      rb[i] = bload(xr, voff, (unsigned)row * xcs4);
+      rb[i] = bload_pol<SGCN_PW_XPOL>(xr, voff, (unsigned)row * xcs4);
       if (MASK) rm[i] = bload(mr, mcol, (unsigned)row * 4u);
       if (XROT) {
         cv += bstep;
@@ -294,7 +303,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
     const unsigned ak0 = AMC ? (unsigned)(k0 * lda * 4) : (unsigned)(k0 * 4);
 #pragma unroll
     for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i)
-      ra[i] = bload(ar, avoff, ak0 + (unsigned)i * astep);
+      ra[i] = bload_pol<SGCN_PW_APOL>(ar, avoff, ak0 + (unsigned)i * astep);
   };
   const int T = p.T;
   auto store_stage = [&](int buf, int k0) {

@@ -547,7 +547,8 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     const int lstep = GR * stride * WP;
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
-      const bool tail = e >= nfull;
+      // (a lane that owns no element, tid >= NTJ, would start one row group past the plane)
+      const bool tail = e >= nfull || !own;
       const int la = tail ? min(la0 + e * lstep, lmax) : la0 + e * lstep;
       emit(e, blend(pl[la], pl[la + 1], pl[la + WP], pl[la + WP + 1], g.dx, g.dy));
     }
@@ -1693,7 +1694,8 @@ int sgcn_tshift_bwd(const float* gout, const float* in, const float* xpos, const
   // <= 64 KiB of LDS); small planes (T = 150 / 75) on 256 threads, so fewer lanes idle per
   // workgroup; anything else takes the global-tap kernel below
   if (stride == 1 && H > 0) {
-    const int nt1 = H * W <= kRaSplit256 ? 256 : kBwdThreads;
+    // (256 threads only where 32 elements per thread cover the plane, as the GBN launcher)
+    const int nt1 = H * W <= kRaSplit256 && ra_lpt(H * W, 256, W) ? 256 : kBwdThreads;
     bool done;
 #define SGCN_RA1(A, R, P)                                                                       done = launch_ra<A, R, P, false, false>(nt1, gout, in, xpos, ypos, in_scale, in_shift,                                                 bn_mean, bn_invstd, gin, pg, bp, B, C, H, W, nullptr,                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,                                           nullptr, st)
     if (bp) {

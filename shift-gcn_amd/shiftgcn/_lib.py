@@ -17,7 +17,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # same-box A/B of two builds (tuning only, e.g. tools/ab_lib.sh): another in-tree build of
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
-ABI_VERSION = 20
+ABI_VERSION = 21
+ABI_DIAG_FLAG = 0x10000   # include/shiftgcn.h SGCN_ABI_DIAG_FLAG: a diagnostic build
 EINVAL = -22
 
 _lib = None
@@ -92,6 +93,28 @@ class NativeLibraryError(RuntimeError):
     pass
 
 
+def _open(path):
+    """dlopen ``path``, check its ABI (refusing a diagnostic build), bind the signatures."""
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    lib.sgcn_abi_version.restype = _I
+    lib.sgcn_abi_version.argtypes = []
+    abi = lib.sgcn_abi_version()
+    if abi & ABI_DIAG_FLAG:
+        # timing probes that drop loads or stores (results are wrong): tools/ only
+        if os.environ.get("SGCN_ALLOW_DIAG_LIB") != "1" or os.path.basename(path) == LIB_NAME:
+            raise NativeLibraryError(
+                f"{path} is a DIAGNOSTIC build (SGCN_PW_DIAG / SGCN_PW_STAMPS / SGCN_DIAG_*: "
+                "its results are wrong); rebuild with `make -C shift-gcn_amd/csrc`")
+        abi &= ~ABI_DIAG_FLAG
+    if abi != ABI_VERSION:
+        raise NativeLibraryError(f"{path}: ABI version {abi} != {ABI_VERSION}; rebuild it")
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
 def load():
     """Return the loaded ctypes library; raise NativeLibraryError when it is absent."""
     global _lib
@@ -101,15 +124,8 @@ def load():
         raise NativeLibraryError(
             f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
             f"g.build()'` (or `make -C shift-gcn_amd/csrc`). There is no CPU fallback.")
-    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
-    for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
-    if lib.sgcn_abi_version() != ABI_VERSION:
-        raise NativeLibraryError("libshiftgcn_hip.so ABI version mismatch; rebuild it")
-    _lib = lib
-    return lib
+    _lib = _open(LIB_PATH)
+    return _lib
 
 
 def check(rc: int, name: str) -> None:

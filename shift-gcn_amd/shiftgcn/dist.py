@@ -75,9 +75,22 @@ def combine_local(grads_per_rank, named, shift_grad_rule: str = "sum"):
 
 
 class GradAllReduce:
-    """Callable run between ``backward()`` and ``optimizer.step()``."""
+    """Callable run between ``backward()`` and ``optimizer.step()``.
 
-    def __init__(self, model: torch.nn.Module, group=None, shift_grad_rule: str = "sum"):
+    The flat bucket IS the gradient storage: every trainable parameter's slot is registered
+    with the HIP path (``ops.register_grad_slots``), whose backward writes each gradient
+    straight into its slot as the tensor autograd then takes as ``.grad`` (no gather into
+    the bucket, no copy back). A ``.grad`` that is not its slot (a gradient torch made, one
+    set by hand, or an accumulation into fresh memory) is copied in, and every ``.grad``
+    is left as its slot. Then ONE all-reduce of the bucket, and the DataParallel scale:
+    applied here (one multiply), or, with ``defer_scale_to`` = a :class:`FusedSGD`, inside
+    that optimizer's update launch (flags bit 1 of ``sgcn_sgd_step``), which also stores the
+    scaled gradient back, so ``.grad`` ends the step holding the same values either way. In
+    the deferred form ``.grad`` holds the rank SUM between this call and ``step()``."""
+
+    def __init__(self, model: torch.nn.Module, group=None, shift_grad_rule: str = "sum",
+                 defer_scale_to=None):
+        from . import ops
         self.group = group
         self.world = dist.get_world_size(group)
         self.named = trainable_named(model)
@@ -85,19 +98,42 @@ class GradAllReduce:
         self.sizes = [p.numel() for _, p in self.named]
         self.total = sum(self.sizes)
         self.scale = reduction_scale(self.named, self.world, shift_grad_rule).to(dev)
+        # per-parameter factor (the rule is per tensor): 1/world, or 1 for summed positions
+        self.param_scale = [1.0 if (is_shift_position(n) and shift_grad_rule == "sum")
+                            else 1.0 / self.world for n, _ in self.named]
         self.flat = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.offsets = ops.register_grad_slots(self.named, self.flat)
+        self.defer_to = defer_scale_to
+        if defer_scale_to is not None and not hasattr(defer_scale_to, "defer_grad_scale"):
+            raise TypeError("defer_scale_to must be a shiftgcn.train.FusedSGD")
+        self.copied = 0   # gradients copied into the bucket by the last call (diagnostics)
 
     def __call__(self):
-        grads = []
-        for _, p in self.named:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            grads.append(p.grad.reshape(-1))
-        torch.cat(grads, out=self.flat)
+        base = self.flat.data_ptr()
+        copied = 0
+        for (_, p), off, k in zip(self.named, self.offsets, self.sizes):
+            g = p.grad
+            if g is not None and g.data_ptr() == base + 4 * off and g.is_contiguous():
+                continue   # written in place by the HIP backward
+            slot = self.flat[off:off + k].view(p.shape)
+            if g is None:
+                slot.zero_()
+            else:
+                slot.copy_(g)
+                copied += 1
+            p.grad = slot
+        self.copied = copied
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.mul_(self.scale)
-        for (_, p), g in zip(self.named, torch.split(self.flat, self.sizes)):
-            p.grad.copy_(g.view_as(p.grad))
+        if self.defer_to is not None:
+            self.defer_to.defer_grad_scale(
+                [(p, s) for (_, p), s in zip(self.named, self.param_scale) if s != 1.0])
+        else:
+            self.flat.mul_(self.scale)
+
+    def close(self):
+        """Unregister the bucket slots (the model's gradients go to fresh memory again)."""
+        from . import ops
+        ops.unregister_grad_slots([p for _, p in self.named])
 
 
 def broadcast_buffers(model: torch.nn.Module, src: int = 0, group=None):

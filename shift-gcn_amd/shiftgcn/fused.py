@@ -107,10 +107,16 @@ def _pos_grads(gx, gy, shift):
     allocated here."""
     if not isinstance(gx, ops.PosPartials):
         return gx, gy
-    ox, oy = torch.empty_like(shift.xpos), torch.empty_like(shift.ypos)
+    ox, oy = ops.grad_like(shift.xpos), ops.grad_like(shift.ypos)
     with _OffPath(True, gx.ws):
         gx.finalize(ox, oy)
     return ox, oy
+
+
+def _pos_alloc(shift, off):
+    """Gradient tensors for a shift backward's (xpos, ypos) gradients (their bucket slots
+    when registered, ops.grad_like), or None when they are deferred to the side stream."""
+    return None if off else (ops.grad_like(shift.xpos), ops.grad_like(shift.ypos))
 
 
 def join_side(device):
@@ -212,8 +218,8 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
         ops.bn_bwd_apply(dH, s.H, True, s.Z, coefZ, 3, dr=g_id, dx=dZ, dy_coef=dy_coef)
     # dZ is stored in Z's pre-shift_out layout, so the einsum/bias grads and dX read it as
     # a plain plane: G(b,d,n) = dZ[b,d,n]
-    dLW = torch.empty_like(mod.Linear_weight)
-    dLb = torch.empty_like(mod.Linear_bias)
+    dLW = ops.grad_like(mod.Linear_weight)
+    dLb = ops.grad_like(mod.Linear_bias)
     dXt = _empty(B, Cin, T, V, like=x0)
     # on the side stream the weight gradient is enqueued after the dX contraction (it then
     # overlaps the streaming passes that follow instead of competing for the MFMA pipes)
@@ -228,13 +234,13 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
                                                               add2_mask=a2m)
     else:
         dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
-    dmask = torch.empty_like(mod.Feature_Mask)
+    dmask = ops.grad_like(mod.Feature_Mask)
     with _OffPath(off, mpart):
         ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V, out=dmask)
     g["Feature_Mask"] = dmask
     if mod.has_down:
-        dWd = torch.empty_like(conv.weight)
-        dbd = torch.empty_like(conv.bias)
+        dWd = ops.grad_like(conv.weight)
+        dbd = ops.grad_like(conv.bias)
         ops.pw_fwd(conv.weight, True, None, PV(dD0), PV(dx), Cin, Cout, T, V, accumulate=True)
         with _OffPath(off, dD0, x0):
             ops.pw_dw(PV(dD0), PV(x0), dWd, Cout, Cin, T, V, dbias=dbd)
@@ -341,14 +347,16 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     # side stream, _pos_grads: the positions' gradients only feed the optimizer)
     if gpre is not None:   # dS = bn2's input gradient, formed inside the shift backward
         dRp, gx, gy = ops.tshift_bwd_bnin(gpre[0], gpre[1], s.S, gpre[2], s.R,
-                                          so.xpos.detach(), so.ypos.detach(), defer_pos=off)
+                                          so.xpos.detach(), so.ypos.detach(), defer_pos=off,
+                                          pos_out=_pos_alloc(so, off))
     else:
         dRp, gx, gy = ops.tshift_bwd(dS, s.R, so.xpos.detach(), so.ypos.detach(), so.stride,
-                                     relu_mask=True, defer_pos=off)
+                                     relu_mask=True, defer_pos=off,
+                                     pos_out=_pos_alloc(so, off))
     g["shift_out.xpos"], g["shift_out.ypos"] = _pos_grads(gx, gy, so)
     tl = mod.temporal_linear
-    dWt = torch.empty_like(tl.weight)
-    dbt = torch.empty_like(tl.bias)
+    dWt = ops.grad_like(tl.weight)
+    dbt = ops.grad_like(tl.bias)
 
     dAs = _empty(B, C, T, V, like=H)
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
@@ -360,13 +368,14 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     if gcn_z is not None and GBN_FUSION and si.stride == 1 and ops.ra_fits(T * V, V):
         down = gcn_z[2] if len(gcn_z) > 2 else None
         res = ops.tshift_bwd_gbn(dAs, H, si.xpos.detach(), si.ypos.detach(), s.ast, gcn_z[0],
-                                 gcn_z[1], defer_pos=off, down=down)
+                                 gcn_z[1], defer_pos=off, down=down,
+                                 pos_out=_pos_alloc(si, off))
         dA, gx, gy, part, zpart = res[:5]
         out["pre6"] = (zpart, s.ast, res[5] if down is not None else None)
     else:
         dA, gx, gy, part = ops.tshift_bwd(
             dAs, H, si.xpos.detach(), si.ypos.detach(), si.stride, scale=s.ast.scale,
-            shift=s.ast.shift, bn_stats=s.ast, defer_pos=off)
+            shift=s.ast.shift, bn_stats=s.ast, defer_pos=off, pos_out=_pos_alloc(si, off))
     g["shift_in.xpos"], g["shift_in.ypos"] = _pos_grads(gx, gy, si)
     coef, g["bn.weight"], g["bn.bias"] = ops.bn_bwd_finalize(part, B, C, B * T * V, s.ast,
                                                              mod.bn)
@@ -405,8 +414,8 @@ def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate, off=False):
     B, Cin, T, V = s.x.shape
     conv = mod.conv
     Cout = conv.out_channels
-    dW = torch.empty_like(conv.weight)
-    db = torch.empty_like(conv.bias)
+    dW = ops.grad_like(conv.weight)
+    db = ops.grad_like(conv.bias)
     ops.pw_fwd(conv.weight, True, None, PV(dRc), PV(dx, mod.stride), Cin, Cout, s.To, V,
                accumulate=accumulate)
     with _OffPath(off, dRc, s.x):

@@ -66,6 +66,42 @@ class _PoolFunction(torch.autograd.Function):
         return ops.pool_bwd(g.contiguous(), ctx.shape, ctx.N, ctx.M), None, None
 
 
+class _LinearSlotsFunction(torch.autograd.Function):
+    """``fc`` (F.linear = addmm(bias, x, weight.t())) whose weight / bias gradients are
+    written into their gradient slots (shiftgcn.dist.GradAllReduce's bucket): the same
+    calls torch's addmm backward makes (mm_mat2_backward for a column-major mat2:
+    ``grad.t().mm(x)``; mm_mat1_backward: ``grad.mm(weight)``; the bias: the sum over the
+    batch), with ``out=`` the slot."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.params = (weight, bias)   # the parameters themselves: their slots and .grad
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        weight, bias = ctx.params
+        dx = g.mm(w) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            dw = ops.grad_like(weight)
+            torch.mm(g.t(), x, out=dw)
+        if bias is not None and ctx.needs_input_grad[2]:
+            db = ops.grad_like(bias)
+            torch.sum(g, 0, out=db)
+        return dx, dw, db
+
+
+def linear(fc, x):
+    """``fc(x)``; through :class:`_LinearSlotsFunction` while fc's weight has a gradient
+    slot (a data-parallel bucket is registered), so its gradients land in the bucket."""
+    if ops.grad_slot(fc.weight) is None or x.dim() != 2:
+        return fc(x)
+    return _LinearSlotsFunction.apply(x, fc.weight, fc.bias)
+
+
 def data_bn_planes(bn, x):
     """(N, C, T, V, M) clip -> data_bn-normalised planes (N*M, C, T, V)."""
     ops.check_input(x, "input")

@@ -92,6 +92,56 @@ def _shp(t):
     return "x".join(map(str, t.shape))
 
 
+# --------------------------------------------------------------------------------------
+# gradient slots: a parameter registered here (shiftgcn.dist.GradAllReduce's flat bucket)
+# gets its gradient written straight into its slot of the bucket, as a fresh view that
+# autograd's AccumulateGrad takes as the parameter's .grad (it steals a gradient nothing
+# else references), so the data-parallel step needs no gather of the gradients into the
+# bucket and no copy back. Only while .grad is None: with an existing .grad (accumulation)
+# the new gradient goes to fresh memory and autograd adds it into .grad as usual.
+# --------------------------------------------------------------------------------------
+from torch.utils.weak import WeakIdKeyDictionary  # noqa: E402
+
+_GRAD_SLOTS = WeakIdKeyDictionary()
+
+
+def register_grad_slots(named, flat):
+    """Map every parameter of ``named`` ([(name, p)], bucket order) to its slot of the
+    1-D ``flat`` fp32 bucket; returns the offsets."""
+    offs, off = [], 0
+    for _, p in named:
+        _GRAD_SLOTS[p] = (flat, off)
+        offs.append(off)
+        off += p.numel()
+    if off != flat.numel():
+        raise ValueError("gradient bucket size does not match the parameters")
+    return offs
+
+
+def unregister_grad_slots(params):
+    for p in params:
+        _GRAD_SLOTS.pop(p, None)
+
+
+def grad_slot(p):
+    """A fresh view of p's bucket slot (p's shape), or None if p has no slot."""
+    s = _GRAD_SLOTS.get(p)
+    if s is None:
+        return None
+    flat, off = s
+    return flat[off:off + p.numel()].view(p.shape)
+
+
+def grad_like(p):
+    """Output tensor for p's gradient: its bucket slot while p.grad is None, else a new
+    tensor like p."""
+    if p.grad is None:
+        v = grad_slot(p)
+        if v is not None:
+            return v
+    return torch.empty_like(p)
+
+
 def _stream(t: torch.Tensor):
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -240,16 +290,23 @@ class PosPartials:
         return gx, gy
 
 
-def _pos_out(defer_pos, ws, B, C, dev):
-    """(gx, gy) tensors for the kernel, or (None, None) + PosPartials when deferred."""
+def _pos_out(defer_pos, ws, B, C, dev, pos_out=None):
+    """(gx, gy) tensors for the kernel (``pos_out`` if given, e.g. gradient slots), or
+    (None, None) + PosPartials when deferred."""
     if defer_pos:
         return None, None, PosPartials(ws, B, C)
+    if pos_out is not None:
+        for t, n in zip(pos_out, ("grad_xpos", "grad_ypos")):
+            check_input(t, n)
+            if t.numel() != C:
+                raise ValueError(f"{n} must hold {C} elements")
+        return pos_out[0], pos_out[1], None
     return (torch.empty((C,), device=dev, dtype=_F32), torch.empty((C,), device=dev, dtype=_F32),
             None)
 
 
 def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=False,
-               ypos_is_raw=True, bn_stats=None, defer_pos=False):
+               ypos_is_raw=True, bn_stats=None, defer_pos=False, pos_out=None):
     """Backward shift: returns (grad_input, grad_xpos, grad_ypos), plus the BatchNorm
     backward partials of ``bn_stats`` (the BN whose output feeds the shift) if given.
     ``defer_pos``: grad_xpos is a PosPartials and grad_ypos None (see PosPartials).
@@ -269,7 +326,7 @@ def tshift_bwd(gout, inp, xpos, ypos, stride, scale=None, shift=None, relu_mask=
     gin = torch.empty_like(inp)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
-    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
+    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev, pos_out)
     bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32) if bn_stats is not None else None
     nb = 4 * (gout.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
@@ -307,7 +364,7 @@ def ra_fits(n, V):
 
 
 def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats", defer_pos=False,
-                   down=None):
+                   down=None, pos_out=None):
     """Shift_tcn.shift_in backward (stride 1, Shift_tcn.bn's affine on the taps and its
     backward partials) that also emits the k-free backward sums of Shift_gcn.bn, whose
     input is ``z`` and whose ReLU output is ``inp`` (sgcn_tshift_bwd_gbn). ``down`` =
@@ -325,7 +382,7 @@ def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats", defe
     gin = torch.empty_like(inp)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
-    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
+    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev, pos_out)
     bpart = torch.empty((B * C * 2,), device=dev, dtype=_F32)
     zpart = torch.empty((6 * B * C * W,), device=dev, dtype=_F32)
     d, dst, dpart = None, None, None
@@ -351,7 +408,7 @@ def tshift_bwd_gbn(gout, inp, xpos, ypos, st: "BnStats", z, zst: "BnStats", defe
 BNIN_MAX_PLANE = 16384   # sgcn_tshift_bwd_bnin: LDS-staged stride-1 planes only
 
 
-def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False):
+def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False, pos_out=None):
     """Stride-1 shift backward (ReLU mask on ``inp``) whose output gradient is the input
     gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3 (s = that
     BatchNorm's input), formed in the kernel. Returns (grad_input, grad_xpos, grad_ypos)."""
@@ -363,7 +420,7 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False):
     gin = torch.empty_like(inp)
     nbytes = lib.sgcn_tshift_bwd_ws_bytes(B, C)
     ws = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=_F32)
-    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev)
+    gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev, pos_out)
     nb = 4 * (3 * dy.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
         rc = lib.sgcn_tshift_bwd_bnin(_ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp),
@@ -611,8 +668,8 @@ def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
     """Returns (coef[3,F], dgamma, dbeta) with dgamma/dbeta in the module's layout."""
     dev = part.device
     coef = torch.empty((3, F), device=dev, dtype=_F32)
-    dgamma = torch.empty_like(bn.weight) if bn.weight is not None else None
-    dbeta = torch.empty_like(bn.bias) if bn.bias is not None else None
+    dgamma = grad_like(bn.weight) if bn.weight is not None else None
+    dbeta = grad_like(bn.bias) if bn.bias is not None else None
     with _timed("finalize", 0, 4 * part.numel(), part):
         rc = _lib.load().sgcn_bn_bwd_finalize(_ptr(part), B, F, int(n_total), perm_V,
                                               _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
@@ -628,8 +685,8 @@ def bn_bwd_finalize_gbn(part6, B, C, V, n_total, dy_coef, dy_st: BnStats, st: Bn
     dev = part6.device
     F = C * V
     coef = torch.empty((3, F), device=dev, dtype=_F32)
-    dgamma = torch.empty_like(bn.weight) if bn.weight is not None else None
-    dbeta = torch.empty_like(bn.bias) if bn.bias is not None else None
+    dgamma = grad_like(bn.weight) if bn.weight is not None else None
+    dbeta = grad_like(bn.bias) if bn.bias is not None else None
     with _timed("finalize", 0, 4 * part6.numel(), part6):
         rc = _lib.load().sgcn_bn_bwd_finalize_gbn(_ptr(part6), B, C, V, int(n_total),
                                                   _ptr(dy_coef), _ptr(dy_st.mean),

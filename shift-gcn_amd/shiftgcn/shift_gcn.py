@@ -206,7 +206,7 @@ class Model(nn.Module):
             for u in units:
                 x = u(x)
         x = head.pool(x, N, M)        # x.view(N, M, C, -1).mean(3).mean(1)  (:211-214)
-        return self.fc(x)
+        return head.linear(self.fc, x)
 
 
 @contextlib.contextmanager

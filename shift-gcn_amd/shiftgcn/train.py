@@ -54,6 +54,13 @@ class FusedSGD(torch.optim.SGD):
         super().__init__(params, lr=lr, momentum=momentum, dampening=dampening,
                          weight_decay=weight_decay, nesterov=nesterov, foreach=True, **kw)
         self._layout = None   # (param signature, device numel / chunk map, n chunks)
+        self._gscale = {}     # id(param) -> (param, gradient scale) for the next step only
+
+    def defer_grad_scale(self, pairs):
+        """[(param, s)]: the next ``step`` first scales these parameters' gradients by s
+        and stores them back (shiftgcn.dist.GradAllReduce's DataParallel 1/world), inside
+        the update launch."""
+        self._gscale = {id(p): (p, float(s)) for p, s in pairs}
 
     def _native_ok(self, items):
         g0 = self.param_groups[0]
@@ -62,9 +69,21 @@ class FusedSGD(torch.optim.SGD):
                     g["dampening"] != 0 or g.get("maximize", False) or
                     g.get("differentiable", False)):
                 return False
-        return all(p.is_cuda and p.dtype == torch.float32 and p.grad.dtype == torch.float32
-                   and not p.grad.is_sparse and p.is_contiguous() and p.grad.is_contiguous()
-                   for p, _ in items) and len({p.device for p, _ in items}) == 1
+        if len({p.device for p, _ in items}) != 1:
+            return False
+        for p, _ in items:
+            if not (p.is_cuda and p.dtype == torch.float32 and p.grad.dtype == torch.float32
+                    and not p.grad.is_sparse and p.is_contiguous() and p.grad.is_contiguous()
+                    and p.grad.device == p.device):
+                return False
+            # an existing momentum buffer goes into the kernel's table as a raw pointer: it
+            # must be a float32 contiguous tensor of p's size ON p's device (e.g. state
+            # loaded before model.cuda() stays on the host; torch's SGD raises there)
+            buf = self.state.get(p, {}).get("momentum_buffer")
+            if buf is not None and not (buf.device == p.device and buf.dtype == torch.float32
+                                        and buf.is_contiguous() and buf.numel() == p.numel()):
+                return False
+        return True
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -72,11 +91,16 @@ class FusedSGD(torch.optim.SGD):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        gscale, self._gscale = self._gscale, {}
         items = [(p, g) for g in self.param_groups for p in g["params"] if p.grad is not None]
         if not items:
             return loss
         if not self._native_ok(items):
-            return super().step()
+            for p, sc in gscale.values():   # the deferred scale as its own multiply
+                if p.grad is not None:
+                    p.grad.mul_(sc)
+            super().step()     # (the closure, if any, was evaluated above)
+            return loss
         import struct
 
         from . import _lib
@@ -107,7 +131,14 @@ class FusedSGD(torch.optim.SGD):
                     st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.preserve_format)
                     first = 1
                 buf = st.get("momentum_buffer") if momentum != 0 else p
-                rows += [p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), wdlr, first]
+                flags = first
+                sc = gscale.get(id(p))
+                if sc is not None and sc[0] is p:
+                    # bit 1 + the float's bits in 32-63 (a signed int64 for the table)
+                    bits = struct.unpack("<I", struct.pack("<f", sc[1]))[0]
+                    flags |= 2 | (bits << 32)
+                    flags = struct.unpack("<q", struct.pack("<Q", flags))[0]
+                rows += [p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), wdlr, flags]
         table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
         rc = lib.sgcn_sgd_step(table.data_ptr(), numel_d.data_ptr(), chunks_d.data_ptr(),
                                nchunks, momentum, int(bool(g0["nesterov"])), _stream(table))

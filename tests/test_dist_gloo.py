@@ -194,3 +194,55 @@ def test_real_model_grad_allreduce_equals_dataparallel_gloo_world2():
         for k, b in ref.named_buffers():
             assert np.array_equal(bufs[k], b.numpy()), (rank, k)
     assert n_shift == 2 * 20   # 2 ranks x 10 units x (shift_in, shift_out)
+
+
+def _defer_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    torch.set_num_threads(1)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shiftgcn.dist import GradAllReduce, broadcast_parameters
+        from shiftgcn.train import FusedSGD
+        out = {}
+        for defer in (False, True):
+            torch.manual_seed(5)
+            m = Toy()
+            broadcast_parameters(m)
+            opt = (FusedSGD if defer else torch.optim.SGD)(
+                [p for p in m.parameters() if p.requires_grad], lr=0.1, momentum=0.9,
+                nesterov=True, weight_decay=1e-4)
+            ga = GradAllReduce(m, defer_scale_to=opt if defer else None)
+            for step in range(2):
+                g = torch.Generator().manual_seed(50 * step + rank)
+                for p in m.parameters():
+                    if p.requires_grad:
+                        p.grad = torch.randn(p.shape, generator=g)
+                ga()
+                # every .grad is its bucket slot after the call
+                base = ga.flat.data_ptr()
+                assert all(p.grad.data_ptr() == base + 4 * off
+                           for (_, p), off in zip(ga.named, ga.offsets))
+                opt.step()
+            ga.close()
+            out[defer] = {n: p.detach().numpy().copy() for n, p in m.named_parameters()
+                          if p.requires_grad}
+            out[(defer, "grad")] = {n: p.grad.numpy().copy() for n, p in m.named_parameters()
+                                    if p.requires_grad}
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_deferred_scale_matches_multiply_then_step_gloo_world2():
+    """GradAllReduce(defer_scale_to=FusedSGD): the DataParallel 1/world applied inside the
+    optimizer step (here the host fallback: one multiply, then torch's update) leaves the
+    same parameters AND the same .grad as the scale applied by GradAllReduce itself."""
+    res = _spawn(_defer_worker)
+    for rank, out in res:
+        for key in (False, (False, "grad")):
+            other = True if key is False else (True, "grad")
+            for n, v in out[key].items():
+                assert np.array_equal(v, out[other][n]), (rank, key, n)

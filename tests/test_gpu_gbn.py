@@ -177,3 +177,38 @@ def test_gbn_down_sums_match_two_pass(case):
     assert _rel(db_new, db_ref) < 1e-5 and _rel(dg_new, dg_ref) < 1e-5
     assert _rel(c_new[0], c_ref[0]) == 0.0
     assert _rel(c_new[1], c_ref[1]) < 1e-5 and _rel(c_new[2], c_ref[2]) < 1e-5
+
+
+# planes the LDS-staged stride-1 backward does not take (W > 64, or more than 16,384
+# floats): sgcn_tshift_bwd falls back to the global-tap kernel, whose BatchNorm partials
+# must read the statistics of the plane's OWN channel (a bug there read them at
+# blockIdx % C, and no test reached this kernel with bn_stats)
+@pytest.mark.parametrize("shape", [(2, 6, 12, 70), (1, 3, 700, 25)],
+                         ids=["W70", "HW17500"])
+def test_global_tap_backward_bn_partials(shape):
+    from shiftgcn import ops
+    B, C, T, V = shape
+    g = torch.Generator().manual_seed(B * 1000 + C * 100 + T + V)
+    H = (torch.randn(B, C, T, V, generator=g) * 1.5 + 0.25).to(DEV)
+    dAs = torch.randn(B, C, T, V, generator=g).to(DEV)
+    xpos = ((torch.rand(C, generator=g) - 0.5) * 2e-8).to(DEV)
+    ypos = ((torch.rand(C, generator=g) - 0.5) * 4).to(DEV)
+    bn = nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g))
+    st = ops.bn_finalize(ops.moments(H, False), B, C, T * V, bn)
+    # distinct per-channel statistics, so reading another channel's shows
+    assert float(st.mean.std()) > 0
+    gin, gx, gy, part = ops.tshift_bwd(dAs, H, xpos, ypos, 1, scale=st.scale, shift=st.shift,
+                                       bn_stats=st)
+    torch.cuda.synchronize()
+    gd = gin.double()
+    xhat = (H.double() - st.mean.double().view(1, C, 1, 1)) * st.invstd.double().view(1, C, 1, 1)
+    ref = torch.stack([gd.sum((2, 3)), (gd * xhat).sum((2, 3))], -1).reshape(-1)
+    assert _rel(part, ref) < 1e-5
+    # the input gradient itself (independent of the affine taps): bit-exact vs the oracle
+    from oracle import shift_oracle as so
+    exp = so.shift_bottom_backward(dAs.cpu().numpy(), xpos.cpu().numpy(), ypos.cpu().numpy(),
+                                   T, 1)
+    assert torch.equal(gin.cpu(), torch.from_numpy(exp))

@@ -106,3 +106,64 @@ def test_model_training_step_with_fused_sgd():
     torch.cuda.synchronize()
     for (n, a), (_, b) in zip(m2.named_parameters(), m1.named_parameters()):
         assert _rel(a.detach(), b.detach()) < 1e-5, n
+
+
+def test_fused_sgd_host_momentum_buffer_is_not_passed_to_the_kernel():
+    """Optimizer state loaded while the parameters were on the host keeps its momentum
+    buffers there after the parameters move to the GPU. The native update must not take
+    those host pointers (the kernel would dereference them); FusedSGD then behaves exactly
+    like torch.optim.SGD (which raises, or updates identically)."""
+    from shiftgcn.train import FusedSGD
+
+    def run(cls):
+        g = torch.Generator().manual_seed(11)
+        ps = [torch.nn.Parameter(torch.randn(s, generator=g)) for s in ((64, 8), (33,))]
+        o = cls(ps, lr=0.1, momentum=0.9, nesterov=True)
+        for p in ps:
+            p.grad = torch.randn(p.shape, generator=g)
+        o.step()                               # host-side momentum buffers
+        for p in ps:                           # the parameters move, the state does not
+            p.data = p.data.to(DEV)
+            p.grad = torch.randn(p.shape, generator=g).to(DEV)
+        assert all(o.state[p]["momentum_buffer"].device.type == "cpu" for p in ps)
+        try:
+            o.step()
+        except RuntimeError as e:
+            return ("raised", type(e))
+        torch.cuda.synchronize()
+        return ("ok", [p.detach().cpu() for p in ps])
+
+    ref, ours = run(torch.optim.SGD), run(FusedSGD)
+    assert ref[0] == ours[0]
+    if ref[0] == "ok":
+        for a, b in zip(ours[1], ref[1]):
+            assert torch.equal(a, b)
+
+
+def test_fused_sgd_deferred_grad_scale_matches_multiply_then_step():
+    """sgcn_sgd_step flags bit 1: grad *= s inside the update (GradAllReduce's deferred
+    DataParallel 1/world), stored back: same parameters, buffers and .grad as a separate
+    multiply followed by the step, bit for bit."""
+    from shiftgcn.train import FusedSGD
+    a = [p.clone().requires_grad_(True) for p in _params(21)]
+    b = [p.clone().requires_grad_(True) for p in _params(21)]
+    oa = FusedSGD(_groups(a, 0.1), lr=0.1, momentum=0.9, nesterov=True)
+    ob = FusedSGD(_groups(b, 0.1), lr=0.1, momentum=0.9, nesterov=True)
+    g = torch.Generator().manual_seed(22)
+    scales = [0.125, 1.0 / 3.0, 0.5, 1.0, 0.25, 1.0 / 7.0]
+    for _ in range(3):
+        grads = [torch.randn(p.shape, generator=g).to(DEV) for p in a]
+        for ps in (a, b):
+            for p, gr in zip(ps, grads):
+                p.grad = gr.clone()
+        with torch.no_grad():
+            for p, s in zip(b, scales):
+                p.grad.mul_(s)
+        oa.defer_grad_scale([(p, s) for p, s in zip(a, scales) if s != 1.0])
+        oa.step()
+        ob.step()
+    torch.cuda.synchronize()
+    for p, q in zip(a, b):
+        assert torch.equal(p, q)
+        assert torch.equal(p.grad, q.grad)
+        assert torch.equal(oa.state[p]["momentum_buffer"], ob.state[q]["momentum_buffer"])

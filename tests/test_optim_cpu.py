@@ -21,3 +21,24 @@ def test_fused_sgd_cpu_falls_back_to_torch():
         ob.step()
     for p, q in zip(a, b):
         assert torch.equal(p, q)
+
+
+def test_fused_sgd_fallback_returns_the_closure_loss():
+    """torch.optim.SGD.step(closure) returns the closure's loss; so must the fallback path
+    (the closure is evaluated once, before the stock update)."""
+    from shiftgcn.train import FusedSGD
+    p = torch.nn.Parameter(torch.ones(4))
+    opt = FusedSGD([p], lr=0.1, momentum=0.9)
+    calls = []
+
+    def closure():
+        calls.append(1)
+        opt.zero_grad()
+        loss = (p * p).sum()
+        loss.backward()
+        return loss
+
+    loss = opt.step(closure)
+    assert loss is not None and float(loss) == 4.0
+    assert len(calls) == 1
+    assert torch.allclose(p.detach(), torch.full((4,), 0.8))
