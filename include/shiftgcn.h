@@ -34,7 +34,8 @@ extern "C" {
  * 20: sgcn_tshift_bwd_gbn also takes the down conv's BatchNorm (d, d_mean, d_invstd,
  * d_part; NULL when the Shift_gcn has none); sgcn_sgd_step (the optimizer update).
  * 21: sgcn_sgd_step's per-tensor gradient scale (flags bit 1 + the float in bits 32-63: the
- * data-parallel reduction's 1/world applied inside the update, written back to the grad). */
+ * data-parallel reduction's 1/world applied inside the update, written back to the grad);
+ * sgcn_pw_fwd_bn_res (the inference Shift_gcn tail in the contraction epilogue). */
 int sgcn_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
@@ -190,6 +191,21 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
                 const float* mask, float* y, long long y_bstride, long long y_cstride,
                 int y_tstride, int y_rsign, int relu, int accumulate, int B, int M, int K,
                 int T, int V, void* stream);
+
+/* Inference Shift_gcn in ONE launch (shift_gcn.py:131-141, BatchNorms in eval mode; round 4):
+ *   H[b][m][out(n,m)] = relu( (sum_k A[m][k] X(b,k,n) + bias[m]) * out_scale[m*V + v'] +
+ *                             out_shift[m*V + v'] + res[b][m][out(n,m)] ),
+ * v' = the stored (shift_out-rotated by y_rsign) joint, res with y's layout (the identity
+ * down = the unit input, or the down conv's output with its BatchNorm folded into the conv
+ * weights). out_scale/out_shift: BatchNorm1d(V*C_out)'s eval apply coefficients in the
+ * natural [channel][joint] order. A as sgcn_pw_fwd; x plain (the gathered, masked gcn
+ * input); the product in the same order as sgcn_tshift_fwd_pre's staging, so H is what that
+ * kernel formed in registers. M, K <= 256. */
+int sgcn_pw_fwd_bn_res(const float* w, int w_mcontig, const float* bias, const float* x,
+                       long long x_bstride, long long x_cstride, const float* out_scale,
+                       const float* out_shift, const float* res, float* y,
+                       long long y_bstride, long long y_cstride, int y_rsign, int B, int M,
+                       int K, int T, int V, void* stream);
 
 /* Shift_tcn's shift_in fused into its temporal_linear (shift_gcn.py:66-70):
  *   Y[b][m][n] = act( sum_k w[m*K + k] * S_k(b, n) + bias[m] ),

@@ -49,6 +49,8 @@ SIGNATURES = {
                                  _P]),
     "sgcn_pw_fwd": (_I, [_P, _I, _P, _P, _L, _L, _I, _I, _P, _P, _L, _L, _I, _I, _I, _I, _I,
                          _I, _I, _I, _I, _P]),
+    "sgcn_pw_fwd_bn_res": (_I, [_P, _I, _P, _P, _L, _L, _P, _P, _P, _P, _L, _L, _I, _I, _I, _I,
+                                _I, _I, _P]),
     "sgcn_pw_tshift_ws_bytes": (_Z, [_I]),
     "sgcn_pw_fwd_tshift": (_I, [_P, _P, _P, _L, _L, _P, _P, _P, _P, _P, _P, _Z, _P, _L, _L, _I,
                                 _I, _I, _I, _I, _I, _P]),

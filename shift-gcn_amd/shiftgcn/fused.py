@@ -261,6 +261,66 @@ def tshift_fused(C):
     return C >= TSHIFT_FUSION_MIN_C
 
 
+def folded_conv_bn(conv, bn):
+    """Eval-mode conv -> BatchNorm with nothing in between (``down`` = Conv2d + BN2d,
+    shift_gcn.py:83-86; ``tcn`` = Conv2d + BN2d, :31-45) folded into ONE conv: weight
+    ``W * s[o]``, bias ``b * s + t`` with the BatchNorm's eval apply coefficients
+    (s = gamma * invstd, t = beta - mean * s, sgcn_bn_eval_coef). Computed once and cached
+    on the conv, keyed by the storage and version counters of every tensor it reads, so an
+    optimizer step, load_state_dict or a device move recomputes it."""
+    srcs = (conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var)
+    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in srcs)
+    key += (float(bn.eps),)
+    c = conv.__dict__.get("_sgcn_fold")
+    if c is not None and c[0] == key:
+        return c[1], c[2]
+    st = ops.bn_eval_coef(bn, conv.out_channels)
+    with torch.no_grad():
+        w = (conv.weight.detach() *
+             st.scale.view(-1, *([1] * (conv.weight.dim() - 1)))).contiguous()
+        b = (conv.bias.detach() * st.scale + st.shift if conv.bias is not None
+             else st.shift.clone())
+    conv.__dict__["_sgcn_fold"] = (key, w, b)
+    return w, b
+
+
+def gcn_infer_h(mod, x0):
+    """Inference Shift_gcn in one contraction launch (sgcn_pw_fwd_bn_res): einsum +
+    Linear_bias, shift_out in the store addresses, BatchNorm1d(V*C) eval, + down (its
+    BatchNorm folded into the conv) or identity, ReLU, all in the epilogue; returns H."""
+    B, Cin, T, V = x0.shape
+    Cout = mod.out_channels
+    cache = mod.__dict__.pop("_gather_cache", None)
+    if cache is not None and cache[0] is x0:
+        xg = cache[1]
+    else:
+        xg = ops.gcn_gather(x0, ops.mask_prep(mod.Feature_Mask))
+    if mod.has_down:
+        w, b = folded_conv_bn(mod.down[0], mod.down[1])
+        res = _empty(B, Cout, T, V, like=x0)
+        ops.pw_fwd(w, False, b, PV(x0), PV(res), Cout, Cin, T, V)
+    else:
+        res = x0
+    zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
+    H = _empty(B, Cout, T, V, like=x0)
+    ops.pw_fwd_bn_res(mod.Linear_weight, True, mod.Linear_bias, PV(xg), zst, res, PV(H, 1, +1),
+                      Cout, Cin, T, V)
+    return H
+
+
+def convbn_infer_folded(mod, x):
+    """Inference residual ``tcn`` (kernel 1, stride s): the conv with its BatchNorm
+    folded in, one contraction; returns its output (no affine left for the consumer)."""
+    B, Cin, T, V = x.shape
+    conv = mod.conv
+    Cout = conv.out_channels
+    To = (T - 1) // mod.stride + 1
+    w, b = folded_conv_bn(conv, mod.bn)
+    R = _empty(B, Cout, To, V, like=x)
+    ops.pw_fwd(w, False, b, PV(x, mod.stride), PV(R), Cout, Cin, To, V)
+    return R
+
+
 def gcn_infer_z(mod, x0):
     """Inference Shift_gcn up to its contraction output: (Z, zst, res, res_stats); the
     BN1d + down/identity + ReLU are applied by the consumer (sgcn_tshift_fwd_pre)."""
@@ -304,7 +364,12 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
         As = ops.tshift_fwd_pre(pre[0], si.xpos.detach(), si.ypos.detach(), si.stride, pre[1],
                                 pre[2], pre[3], ast)
         ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
-    elif tshift_fused(C):
+    elif tail is not None and C >= EVAL_TSHIFT_FUSION_MIN_C:
+        # inference: shift_in (with bn's eval affine) formed in temporal_linear's operand
+        # staging; the shifted operand is neither stored nor read back
+        ops.pw_fwd_tshift(tl.weight, tl.bias, PV(H), si.xpos.detach(), si.ypos.detach(), ast,
+                          PV(R), Cout, C, T, V, relu=True)
+    elif tshift_fused(C) and tail is None:
         # shift_in (with Shift_tcn.bn's apply) formed in the contraction's operand staging,
         # never read back; also stored from the same registers for the weight gradient
         As = torch.empty_like(H)
@@ -436,14 +501,21 @@ def unit_forward(unit, x, training):
             x.shape[2] * x.shape[3] <= ops.TAIL_MAX_PLANE):
         # inference (no backward can follow): the Shift_gcn tail is fused into shift_in,
         # the unit tail into shift_out; neither H nor S is written
-        pre = gcn_infer_z(unit.gcn1, x)
+        H = pre = None
+        if EVAL_GCN_EPI:   # the Shift_gcn tail in its contraction's epilogue
+            H = gcn_infer_h(unit.gcn1, x)
+        else:              # ... in the shift_in launch's staging (round-1 form)
+            pre = gcn_infer_z(unit.gcn1, x)
         r = rst = None
         if unit.residual_kind == "conv":
-            r, rst, _ = convbn_core_forward(unit.residual, x, training)
+            if EVAL_GCN_EPI:
+                r = convbn_infer_folded(unit.residual, x)
+            else:
+                r, rst, _ = convbn_core_forward(unit.residual, x, training)
         elif unit.residual_kind == "identity":
             r = x
         gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
-        out, xg_next = tcn_core_forward(unit.tcn1, None, training, tail=(r, rst, gm),
+        out, xg_next = tcn_core_forward(unit.tcn1, H, training, tail=(r, rst, gm),
                                         pre=pre)
         if gm is not None:
             consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
@@ -611,6 +683,15 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
 # two-launch form is faster at C = 256 too (+0.5 % same-box, profiles/r03_tsh/), so by
 # default no unit fuses (512 exceeds every Shift-GCN width). A/B knob (0 = every unit).
 TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "512"))
+# Inference (no backward possible, eval mode) unit recipe, round 4: 1 = the Shift_gcn tail
+# (BatchNorm1d eval + down with its BatchNorm folded / identity + ReLU) in the gcn
+# contraction's epilogue (sgcn_pw_fwd_bn_res) and the residual tcn's BatchNorm folded into
+# its conv; 0 = the round-1 form (Z stored, the tail formed in the shift_in launch). A/B knob.
+EVAL_GCN_EPI = int(os.environ.get("SGCN_EVAL_GCN_EPI", "1"))
+# Inference: Shift_tcn's shift_in (+ bn eval affine) formed inside temporal_linear's operand
+# staging (sgcn_pw_fwd_tshift, no side output) from this many input channels up; needs
+# EVAL_GCN_EPI (H materialised). A/B knob.
+EVAL_TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_EVAL_TSHIFT_FUSION_MIN_C", "512"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
 # (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass: 2 = every unit (with a
 # down conv, the down BatchNorm's sums too; round 3), 1 = units without a down conv only

@@ -524,6 +524,36 @@ def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=Fals
     return dw
 
 
+def pw_fwd_bn_res(w, w_mcontig, bias, x: PlaneView, st, res, out: PlaneView, M, K, T, V):
+    """Inference Shift_gcn (sgcn_pw_fwd_bn_res): out = relu((w @ x + bias) * st.scale +
+    st.shift + res) with the per-(channel, stored joint) eval coefficients of its
+    BatchNorm1d(V*C) (``st`` from bn_eval_coef(..., perm_V=V)) and the residual ``res``
+    (out's layout) read at the stored address."""
+    check_input(w, "weight")
+    _opt(bias, "bias")
+    check_input(res, "residual")
+    if x.tstride != 1 or x.rsign != 0 or out.tstride != 1:
+        raise ValueError("pw_fwd_bn_res: plain input planes, unit time stride")
+    if res.shape != out.t.shape or res.stride() != out.t.stride():
+        raise ValueError("pw_fwd_bn_res: the residual must have the output's layout")
+    B = x.t.shape[0]
+    lib = _lib.load()
+    P = B * T * V
+    bc = _batch_chunk([(x, K), (out, M)], B, T, V)
+    with _timed("pw_fwd", 2.0 * P * M * K, 4.0 * P * (2 * M + K), x.t,
+                f"EPI M{M} K{K} T{T} V{V} yrot{out.rsign} mc{int(w_mcontig)}"):
+        for b0 in range(0, B, bc):
+            nb = min(bc, B - b0)
+            rc = lib.sgcn_pw_fwd_bn_res(_ptr(w), int(w_mcontig), _ptr(bias),
+                                        x.t.data_ptr() + 4 * b0 * x.bstride, x.bstride,
+                                        x.cstride, _ptr(st.scale), _ptr(st.shift),
+                                        res.data_ptr() + 4 * b0 * out.bstride,
+                                        out.t.data_ptr() + 4 * b0 * out.bstride, out.bstride,
+                                        out.cstride, out.rsign, nb, M, K, T, V, _stream(x.t))
+            _lib.check(rc, "sgcn_pw_fwd_bn_res")
+    return out.t
+
+
 def pw_fwd_tshift(w, bias, x: PlaneView, xpos, ypos, st, out: PlaneView, M, K, T, V,
                   relu=False, x_shifted=None):
     """Shift_tcn's shift_in fused into temporal_linear (sgcn_pw_fwd_tshift):

@@ -93,14 +93,27 @@ def test_ensemble_graph_replay_matches_eager():
         assert torch.equal(s_g, s_eager) and torch.equal(l_g, l_eager)
 
 
+# inference recipes (shiftgcn.fused knobs): (EVAL_GCN_EPI, EVAL_TSHIFT_FUSION_MIN_C)
+RECIPES = {"pre-staged": (0, 512), "gcn-epilogue": (1, 512), "epilogue+tshift-fused": (1, 0)}
+
+
+@pytest.mark.parametrize("recipe", list(RECIPES))
 @pytest.mark.parametrize("cin,cout,stride,residual,V", [(3, 64, 1, False, 25),
                                                         (64, 64, 1, True, 33),
                                                         (64, 128, 2, True, 25),
                                                         (128, 256, 2, True, 33)])
-def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V):
-    """The no-backward recipe (Shift_gcn tail staged into shift_in, unit tail in the
-    shift_out store, next-unit gather) equals the eval recipe a backward would use."""
+def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V, recipe,
+                                             monkeypatch):
+    """The no-backward recipes (round 1: Shift_gcn tail staged into shift_in; round 4: that
+    tail in the gcn contraction's epilogue with the down / residual BatchNorms folded into
+    their convs, optionally shift_in formed inside temporal_linear's staging; always the unit
+    tail in the shift_out store and the next-unit gather) equal the eval recipe a backward
+    would use."""
     import shiftgcn
+    from shiftgcn import fused
+    epi, minc = RECIPES[recipe]
+    monkeypatch.setattr(fused, "EVAL_GCN_EPI", epi)
+    monkeypatch.setattr(fused, "EVAL_TSHIFT_FUSION_MIN_C", minc)
     torch.manual_seed(3)
     u = shiftgcn.TCN_GCN_unit(cin, cout, None, stride=stride, residual=residual,
                               num_point=V)
@@ -113,3 +126,67 @@ def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V):
     ref = u(xr).detach()
     err = (fused - ref).abs().max().item()
     assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
+
+
+def test_folded_conv_bn_tracks_parameter_and_statistics_updates():
+    """The eval fold of down.1 into down.0 (and residual.bn into residual.conv) is cached
+    per tensor version: in-place changes of the running statistics or of the conv weight
+    (optimizer steps, load_state_dict) are seen by the next inference call."""
+    import shiftgcn
+    from shiftgcn import fused
+    u = shiftgcn.TCN_GCN_unit(64, 128, None, stride=2, residual=True, num_point=25)
+    formula.fill_state(u, seed=77)
+    u = u.to(DEV).eval()
+    x = formula.tensor((2, 64, 16, 25), 78, 1.0).to(DEV)
+
+    def check():
+        with torch.no_grad():
+            fast = u(x)
+        ref = u(x.clone().requires_grad_(True)).detach()
+        err = (fast - ref).abs().max().item()
+        assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
+        return fast
+
+    assert fused.EVAL_GCN_EPI
+    y0 = check()
+    with torch.no_grad():
+        u.gcn1.down[1].running_var.mul_(3.0)
+        u.residual.bn.running_mean.add_(0.25)
+    y1 = check()
+    assert not torch.equal(y0, y1)
+    with torch.no_grad():
+        u.gcn1.down[0].weight.mul_(-0.5)
+    check()
+
+
+@pytest.mark.parametrize("M,K,T,V,rsign", [(64, 64, 20, 25, 1), (128, 64, 12, 33, 1),
+                                           (256, 128, 9, 25, 1), (64, 3, 7, 25, 0)])
+def test_pw_fwd_bn_res_matches_torch(M, K, T, V, rsign):
+    """sgcn_pw_fwd_bn_res vs an fp64 torch evaluation: relu((W x + b) * s[m, v'] + t[m, v']
+    + res) with v' the stored (shift_out-rotated) joint."""
+    from shiftgcn import ops
+    g = torch.Generator().manual_seed(M + K + T + V)
+    B = 3
+    x = torch.randn(B, K, T, V, generator=g)
+    w = torch.randn(K, M, generator=g) / K ** 0.5          # Linear_weight (C_in, C_out)
+    b = torch.randn(M, generator=g)
+    sc = torch.rand(M * V, generator=g) + 0.5
+    sh = torch.randn(M * V, generator=g)
+    res = torch.randn(B, M, T, V, generator=g)
+
+    class St:
+        pass
+    st = St()
+    st.scale, st.shift = sc.to(DEV), sh.to(DEV)
+    y = torch.empty(B, M, T, V, device=DEV)
+    ops.pw_fwd_bn_res(w.to(DEV), True, b.to(DEV), ops.PlaneView(x.to(DEV)), st, res.to(DEV),
+                      ops.PlaneView(y, 1, rsign), M, K, T, V)
+    z = torch.einsum("bktv,km->bmtv", x.double(), w.double()) + b.double().view(1, M, 1, 1)
+    # store joint v' = (v + rsign*m) mod V
+    vv = (torch.arange(V).view(1, V) + rsign * torch.arange(M).view(M, 1)) % V   # [m, v]
+    zr = torch.zeros_like(z)
+    zr.scatter_(3, vv.view(1, M, 1, V).expand(B, M, T, V), z)
+    ref = torch.relu(zr * sc.double().view(1, M, 1, V) + sh.double().view(1, M, 1, V)
+                     + res.double())
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-5 * max(1.0, ref.abs().max().item()), err
