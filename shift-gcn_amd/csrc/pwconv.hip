@@ -124,6 +124,22 @@ __device__ unsigned long long* g_pw_where;
 #define SGCN_PW_APOL 0
 #endif
 
+// XCD-aware tile order (cdna_hip_programming.md T1): workgroups are dealt round-robin over
+// the 8 XCDs, each with its own L2. Consecutive position tiles share the 128-B lines at
+// their edges (a tile's row segment is BN*4 bytes at an arbitrary 4-B alignment: planes are
+// T*V floats), so tile i and i+1 on different XCDs fetch those lines twice (PMC, forward
+// contraction: 1.12x the operand bytes at BN = 256, 1.28-1.30x at BN = 128,
+// profiles/r04_ofetch/). Remapped, the workgroups of one XCD take one contiguous run of
+// tiles (bijective for any count). Speed only.
+#ifndef SGCN_PW_XCD
+#define SGCN_PW_XCD 1
+#endif
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+  if (!SGCN_PW_XCD || n <= 8) return b;
+  const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 __device__ __forceinline__ int pmod(int a, int V) {
   int r = a % V;
   return r < 0 ? r + V : r;
@@ -230,7 +246,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int V = p.V, N = p.T * V, K = p.K, M = p.M;
   const int P = p.B * N;                 // < 2^31 (host-checked)
-  const int p0 = blockIdx.x * BN;
+  const int p0 = xcd_tile(blockIdx.x, gridDim.x) * BN;
   const int m0 = blockIdx.y * BM;
   const auto xr = make_rsrc(p.x.ptr, p.x_bytes);
   const auto ar = make_rsrc(p.A, p.a_bytes);
@@ -426,12 +442,56 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   }
   const bool rotated = p.y.rsign != 0;
   const auto err = make_rsrc(EPI ? p.er : p.y.ptr, EPI ? p.er_bytes : 0u);
+  const unsigned tab_bytes = EPI ? (unsigned)(M * V * 4) : 0u;
+  const auto esr = make_rsrc(EPI ? p.es : p.y.ptr, tab_bytes);
+  const auto etr = make_rsrc(EPI ? p.et : p.y.ptr, tab_bytes);
+  constexpr int RPW = RB / NW;     // rows per wave per pass
+  static_assert(RB % NW == 0, "rows per wave");
+  // the global loads an output element needs besides the accumulator (EPI: its two
+  // BatchNorm coefficients and the residual; ACCUM: the old value) are issued for all of
+  // this wave's rows of a pass BEFORE the pass's LDS staging: in the store loop they would
+  // each wait a memory round trip (a load after the previous row's stores)
+  constexpr int NPF = EPI ? 3 : (ACCUM ? 1 : 0);
+  float pf[NPF ? RPW : 1][NPF ? CQ : 1][NPF ? NPF : 1];
+  auto row_of = [&](int i, int h, int k) {   // (tile row, its store row offset)
+    const int lr = wid + k * NW;
+    return (lr >> 4) * (BM / WM) + i * 32 + 16 * h + (lr & 15);   // uniform
+  };
+  auto voff_of = [&](int trow, int q) {
+    int vo = vq[q];
+    if (rotated) {   // shift_out rotation of the stored joint
+      vo += rot_s[trow];
+      vo = vo >= V ? vo - V : vo;
+    }
+    return vo;
+  };
   auto epilogue = [&](auto relu_tag) {
     constexpr bool RELU = decltype(relu_tag)::value;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
+        if (NPF) {
+#pragma unroll
+          for (int k = 0; k < RPW; ++k) {
+            const int trow = row_of(i, h, k);
+            // a row past M: every address past its extent (loads 0, nothing stored later)
+            const unsigned soff = m0 + trow < M ? (unsigned)(m0 + trow) * ycs4 : p.y_bytes;
+            const unsigned toff = m0 + trow < M ? (unsigned)((m0 + trow) * V) * 4u : tab_bytes;
+#pragma unroll
+            for (int q = 0; q < CQ; ++q) {
+              const int vo = voff_of(trow, q);
+              const unsigned voff = ycolq[q] + (unsigned)(vo * 4);
+              if constexpr (EPI) {
+                pf[k][q][0] = bload(esr, (unsigned)vo * 4u, toff);
+                pf[k][q][1] = bload(etr, (unsigned)vo * 4u, toff);
+                pf[k][q][2] = bload(err, voff, soff);
+              } else if constexpr (ACCUM) {
+                pf[k][q][0] = bload(yr, voff, soff);
+              }
+            }
+          }
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -441,31 +501,25 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
             smem[lr * BN + wn * (BN / WN) + j * 32 + cl] = acc[i][j][r];
           }
         __syncthreads();
-        for (int lr = wid; lr < RB; lr += NW) {
-          const int trow = (lr >> 4) * (BM / WM) + i * 32 + 16 * h + (lr & 15);   // uniform
-          if (m0 + trow >= M) break;   // rows past M (lr increases with trow)
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+          const int lr = wid + k * NW;
+          const int trow = row_of(i, h, k);
+          if (m0 + trow >= M) break;   // rows past M (they increase with k)
           const float bv = bias_s[trow];
-          const int rot = rot_s[trow];
           const unsigned soff = (unsigned)(m0 + trow) * ycs4;
-          const float* __restrict__ esr = EPI ? p.es + (size_t)(m0 + trow) * V : nullptr;
-          const float* __restrict__ etr = EPI ? p.et + (size_t)(m0 + trow) * V : nullptr;
 #pragma unroll
           for (int q = 0; q < CQ; ++q) {
-            int vo = vq[q];
-            if (rotated) {   // shift_out rotation of the stored joint
-              vo += rot;
-              vo = vo >= V ? vo - V : vo;
-            }
-            const unsigned voff = ycolq[q] + (unsigned)(vo * 4);
+            const unsigned voff = ycolq[q] + (unsigned)(voff_of(trow, q) * 4);
             float val = smem[lr * BN + lane + 64 * q] + bv;
-            if (EPI) {
+            if constexpr (EPI) {
               // BatchNorm1d(V*C) eval coefficients of the stored (channel, joint), the
               // residual at the stored address, ReLU (shift_gcn.py:137-141)
-              val = epi_tail(val, esr[vo], etr[vo], bload(err, voff, soff));
+              val = epi_tail(val, pf[k][q][0], pf[k][q][1], pf[k][q][2]);
             } else if (RELU) {
               val = fmaxf(val, 0.f);
             }
-            if (ACCUM) val += bload(yr, voff, soff);
+            if constexpr (ACCUM) val += pf[k][q][0];
             bstore(yr, val, voff, soff);
           }
         }
@@ -680,8 +734,12 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int ntn = (p.Nc + BN - 1) / BN;
-  const int m0 = (blockIdx.x / ntn) * BM, c0 = (blockIdx.x % ntn) * BN;
-  const int split = blockIdx.y;
+  // XCD-aware: one XCD's workgroups take consecutive (split, tile) pairs, i.e. adjacent
+  // position ranges, whose edge lines they then share in one L2 (see xcd_tile)
+  const int lin = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tix = lin % gridDim.x;
+  const int m0 = (tix / ntn) * BM, c0 = (tix % ntn) * BN;
+  const int split = lin / gridDim.x;
   const int V = p.V, T = p.T, N = T * V;
   const int P = p.B * N;
   const int nch = (P + BKP - 1) / BKP;
@@ -817,7 +875,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
         if (m < p.M && c < p.Nc) slab[(size_t)m * p.Nc + c] = acc[i][j][r];
       }
   }
-  if (BIAS && (blockIdx.x % ntn) == 0) {
+  if (BIAS && (tix % ntn) == 0) {
     // row rw + rsub + i*RSTEP is shared by the BKP lanes with equal rsub
 #pragma unroll
     for (int i = 0; i < G_PER; ++i) {

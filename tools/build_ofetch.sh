@@ -9,5 +9,6 @@ $H -DSGCN_PW_DIAG=1 $S -o $ROOT/tools/bench/bin/ofetch_d1 &
 $H -DSGCN_PW_DIAG=2 $S -o $ROOT/tools/bench/bin/ofetch_d2 &
 $H -DSGCN_PW_XPOL=2 $S -o $ROOT/tools/bench/bin/ofetch_xnt &
 $H -DSGCN_PW_APOL=16 $S -o $ROOT/tools/bench/bin/ofetch_asc1 &
+$H -DSGCN_PW_XCD=0 $S -o $ROOT/tools/bench/bin/ofetch_noxcd &
 wait
 ls -la $ROOT/tools/bench/bin/ofetch_*
