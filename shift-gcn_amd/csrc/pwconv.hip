@@ -134,8 +134,12 @@ __device__ unsigned long long* g_pw_where;
 #ifndef SGCN_PW_XCD
 #define SGCN_PW_XCD 1
 #endif
+#ifndef SGCN_DW_XCD
+#define SGCN_DW_XCD 1
+#endif
+template <bool ON = true>
 __device__ __forceinline__ int xcd_tile(int b, int n) {
-  if (!SGCN_PW_XCD || n <= 8) return b;
+  if (!ON || n <= 8) return b;
   const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
@@ -246,7 +250,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int V = p.V, N = p.T * V, K = p.K, M = p.M;
   const int P = p.B * N;                 // < 2^31 (host-checked)
-  const int p0 = xcd_tile(blockIdx.x, gridDim.x) * BN;
+  const int p0 = xcd_tile<SGCN_PW_XCD>(blockIdx.x, gridDim.x) * BN;
   const int m0 = blockIdx.y * BM;
   const auto xr = make_rsrc(p.x.ptr, p.x_bytes);
   const auto ar = make_rsrc(p.A, p.a_bytes);
@@ -736,7 +740,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw3_kernel(DwArgs p) {
   const int ntn = (p.Nc + BN - 1) / BN;
   // XCD-aware: one XCD's workgroups take consecutive (split, tile) pairs, i.e. adjacent
   // position ranges, whose edge lines they then share in one L2 (see xcd_tile)
-  const int lin = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int lin = xcd_tile<SGCN_DW_XCD>(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int tix = lin % gridDim.x;
   const int m0 = (tix / ntn) * BM, c0 = (tix % ntn) * BN;
   const int split = lin / gridDim.x;
