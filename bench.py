@@ -281,6 +281,23 @@ def main():
             return train.train_step(model, opt, xb, yb, grad_sync=sync)
         return train.train_step(model, opt, x, label, grad_sync=sync)
 
+    main_ctx = None
+    if os.environ.get("SGCN_MAIN_CUS_EXCLUDE_SIDE") == "1":
+        # A/B knob: the whole step on a CU-masked stream over the CUs the (CU-masked) side
+        # stream does not use
+        import ctypes
+
+        from shiftgcn import _lib, fused
+        total = ctypes.c_int(0)
+        _lib.check(_lib.load().sgcn_device_cu_count(dev.index or 0, ctypes.byref(total)),
+                   "sgcn_device_cu_count")
+        side = set(fused.cu_mask_bits(total.value, fused.SIDE_CUS, fused.SIDE_CU_PATTERN)
+                   if fused.SIDE_CUS > 0 else [])
+        ms = fused.masked_stream(dev, [c for c in range(total.value) if c not in side])
+        ms.wait_stream(torch.cuda.current_stream(dev))
+        main_ctx = torch.cuda.stream(ms)
+        main_ctx.__enter__()
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

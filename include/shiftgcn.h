@@ -429,6 +429,16 @@ int sgcn_sgd_chunk_elems(void);
 int sgcn_sgd_step(const void* table, const int* numel, const int* chunks, int n_chunks,
                   float momentum, int nesterov, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * CU-masked streams (hipExtStreamCreateWithCUMask), round 4: the weight-gradient side
+ * stream confined to a subset of the CUs. mask: `words` uint32, bit i = CU i of the
+ * device's multiProcessorCount CUs.
+ * ------------------------------------------------------------------------------------ */
+int sgcn_device_cu_count(int device, int* count);
+int sgcn_stream_create_cu_mask(const unsigned* mask, int words, void** stream);
+int sgcn_stream_get_cu_mask(void* stream, unsigned* mask, int words);
+int sgcn_stream_destroy(void* stream);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

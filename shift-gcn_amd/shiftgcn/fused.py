@@ -51,12 +51,62 @@ def _empty(*shape, like):
 # current stream before returning, so everything after loss.backward() sees finished grads.
 # --------------------------------------------------------------------------------------
 _SIDE = {}
+_MASKED = []   # keeps the CU-masked HIP streams alive for the process
+
+
+def cu_mask_bits(total, n, pattern):
+    """CU indices of an n-CU subset of ``total``: "low" = 0..n-1, "high" = the last n,
+    "spread" = every (total/n)-th."""
+    n = max(1, min(n, total))
+    if pattern == "high":
+        return list(range(total - n, total))
+    if pattern == "spread":
+        step = total / n
+        return sorted({int(i * step) for i in range(n)})
+    return list(range(n))
+
+
+def masked_stream(device, cus):
+    """A torch stream over a HIP stream restricted to the CU indices ``cus``
+    (sgcn_stream_create_cu_mask)."""
+    import ctypes
+
+    from . import _lib
+    lib = _lib.load()
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    total = ctypes.c_int(0)
+    _lib.check(lib.sgcn_device_cu_count(idx, ctypes.byref(total)), "sgcn_device_cu_count")
+    words = (total.value + 31) // 32
+    mask = (ctypes.c_uint * words)()
+    for c in cus:
+        if 0 <= c < total.value:
+            mask[c // 32] |= 1 << (c % 32)
+    ptr = ctypes.c_void_p()
+    with torch.cuda.device(idx):
+        _lib.check(lib.sgcn_stream_create_cu_mask(mask, words, ctypes.byref(ptr)),
+                   "sgcn_stream_create_cu_mask")
+    st = torch.cuda.ExternalStream(ptr.value, device=dev)
+    _MASKED.append(st)
+    return st
 
 
 def _side_stream(device):
     s = _SIDE.get(device)
     if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device=device)
+        if SIDE_CUS > 0:   # the side stream confined to SIDE_CUS CUs (A/B knob)
+            import ctypes
+
+            from . import _lib
+            total = ctypes.c_int(0)
+            dev = torch.device(device)
+            _lib.check(_lib.load().sgcn_device_cu_count(
+                dev.index if dev.index is not None else torch.cuda.current_device(),
+                ctypes.byref(total)), "sgcn_device_cu_count")
+            s = masked_stream(device, cu_mask_bits(total.value, SIDE_CUS, SIDE_CU_PATTERN))
+        else:
+            s = torch.cuda.Stream(device=device)
+        _SIDE[device] = s
     return s
 
 
@@ -702,6 +752,10 @@ GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "2"))
 # gradient finalizes, the next unit's mask and the forward's down / residual conv branches.
 # SGCN_ASYNC_DW=0 serializes everything (bench.py's roofline steps, A/B).
 ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
+# The side stream on a CU-masked HIP stream of this many CUs (0 = an ordinary stream, all
+# CUs), chosen by SGCN_SIDE_CU_PATTERN (low / high / spread). A/B knob (round 4).
+SIDE_CUS = int(os.environ.get("SGCN_SIDE_CUS", "0"))
+SIDE_CU_PATTERN = os.environ.get("SGCN_SIDE_CU_PATTERN", "low")
 
 
 def trainable(module):
