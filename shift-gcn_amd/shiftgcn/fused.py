@@ -387,6 +387,10 @@ def gcn_infer_z(mod, x0):
     if mod.has_down:
         conv, bn = mod.down[0], mod.down[1]
         D0 = _empty(B, Cout, T, V, like=x0)
+        if EVAL_FOLD:   # down.1 folded into down.0: the residual needs no affine
+            w, b = folded_conv_bn(conv, bn)
+            ops.pw_fwd(w, False, b, PV(x0), PV(D0), Cout, Cin, T, V)
+            return Z, zst, D0, None
         ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
         return Z, zst, D0, ops.bn_eval_coef(bn, Cout)
     return Z, zst, x0, None
@@ -558,7 +562,7 @@ def unit_forward(unit, x, training):
             pre = gcn_infer_z(unit.gcn1, x)
         r = rst = None
         if unit.residual_kind == "conv":
-            if EVAL_GCN_EPI:
+            if EVAL_FOLD or EVAL_GCN_EPI:
                 r = convbn_infer_folded(unit.residual, x)
             else:
                 r, rst, _ = convbn_core_forward(unit.residual, x, training)
@@ -737,7 +741,11 @@ TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "512"))
 # (BatchNorm1d eval + down with its BatchNorm folded / identity + ReLU) in the gcn
 # contraction's epilogue (sgcn_pw_fwd_bn_res) and the residual tcn's BatchNorm folded into
 # its conv; 0 = the round-1 form (Z stored, the tail formed in the shift_in launch). A/B knob.
-EVAL_GCN_EPI = int(os.environ.get("SGCN_EVAL_GCN_EPI", "1"))
+EVAL_GCN_EPI = int(os.environ.get("SGCN_EVAL_GCN_EPI", "0"))
+# Inference: the eval-mode BatchNorm right after a conv (down.1 after down.0, residual.bn
+# after residual.conv) folded into that conv's weights and bias (folded_conv_bn), so the
+# consumer adds the residual without an affine. A/B knob (round 4).
+EVAL_FOLD = int(os.environ.get("SGCN_EVAL_FOLD", "1"))
 # Inference: Shift_tcn's shift_in (+ bn eval affine) formed inside temporal_linear's operand
 # staging (sgcn_pw_fwd_tshift, no side output) from this many input channels up; needs
 # EVAL_GCN_EPI (H materialised). A/B knob.

@@ -94,7 +94,9 @@ def test_ensemble_graph_replay_matches_eager():
 
 
 # inference recipes (shiftgcn.fused knobs): (EVAL_GCN_EPI, EVAL_TSHIFT_FUSION_MIN_C)
-RECIPES = {"pre-staged": (0, 512), "gcn-epilogue": (1, 512), "epilogue+tshift-fused": (1, 0)}
+# (EVAL_GCN_EPI, EVAL_TSHIFT_FUSION_MIN_C, EVAL_FOLD)
+RECIPES = {"pre-staged": (0, 512, 0), "pre-staged+fold": (0, 512, 1),
+           "gcn-epilogue": (1, 512, 1), "epilogue+tshift-fused": (1, 0, 1)}
 
 
 @pytest.mark.parametrize("recipe", list(RECIPES))
@@ -111,9 +113,10 @@ def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V, rec
     would use."""
     import shiftgcn
     from shiftgcn import fused
-    epi, minc = RECIPES[recipe]
+    epi, minc, fold = RECIPES[recipe]
     monkeypatch.setattr(fused, "EVAL_GCN_EPI", epi)
     monkeypatch.setattr(fused, "EVAL_TSHIFT_FUSION_MIN_C", minc)
+    monkeypatch.setattr(fused, "EVAL_FOLD", fold)
     torch.manual_seed(3)
     u = shiftgcn.TCN_GCN_unit(cin, cout, None, stride=stride, residual=residual,
                               num_point=V)
@@ -128,7 +131,8 @@ def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V, rec
     assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
 
 
-def test_folded_conv_bn_tracks_parameter_and_statistics_updates():
+@pytest.mark.parametrize("epi", [0, 1])
+def test_folded_conv_bn_tracks_parameter_and_statistics_updates(epi, monkeypatch):
     """The eval fold of down.1 into down.0 (and residual.bn into residual.conv) is cached
     per tensor version: in-place changes of the running statistics or of the conv weight
     (optimizer steps, load_state_dict) are seen by the next inference call."""
@@ -147,7 +151,8 @@ def test_folded_conv_bn_tracks_parameter_and_statistics_updates():
         assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
         return fast
 
-    assert fused.EVAL_GCN_EPI
+    monkeypatch.setattr(fused, "EVAL_GCN_EPI", epi)
+    monkeypatch.setattr(fused, "EVAL_FOLD", 1)
     y0 = check()
     with torch.no_grad():
         u.gcn1.down[1].running_var.mul_(3.0)
