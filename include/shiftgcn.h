@@ -264,6 +264,36 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
  * mean, invstd, scale = gamma*invstd, shift = beta - mean*scale (all [F], local feature
  * order); updates running_mean/var (momentum, unbiased var) and num_batches (+1) when
  * non-NULL, in the reference feature order (perm_V > 0: per-joint mapping). */
+/* A training-mode per-channel BatchNorm finalize FOLDED into its first consumer (round 4):
+ * the consumer's (sample, channel) plane workgroups each merge their channel's B partials
+ * (sgcn_moments / sgcn_tshift_fwd plane_stats layout, (B*C) float2 {mean, M2} over n_part
+ * elements each) in sgcn_bn_finalize's order, so the coefficients are bit-identical to
+ * that kernel's; the workgroup of sample 0 writes mean/invstd/scale/shift (C each) and
+ * updates the running statistics (gamma/beta NULL = 1/0; running_* NULL = not tracked;
+ * num_batches += 1 once). Consumers: sgcn_tshift_fwd_fold, sgcn_bn_apply_fold. */
+typedef struct sgcn_bn_fold {
+  const void* part;
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  long long* num_batches;
+  float* mean;
+  float* invstd;
+  float* scale;
+  float* shift;
+  int n_part;
+  float eps;
+  float momentum;
+} sgcn_bn_fold;
+
+/* sgcn_tshift_fwd with the input affine (in_scale/in_shift) of a folded finalize: `fold`
+ * (NULL = no affine) writes fold->mean/invstd/scale/shift (C). Planes the padded LDS
+ * kernel does not take run the finalize as its own launch first (same values). */
+int sgcn_tshift_fwd_fold(const float* in, float* out, const float* xpos, const float* ypos,
+                         const sgcn_bn_fold* fold, float* plane_stats, int B, int C, int H,
+                         int W, int stride, int ypos_is_raw, void* stream);
+
 int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
                      const float* gamma, const float* beta, float eps, float momentum,
                      float* running_mean, float* running_var, long long* num_batches,
@@ -285,6 +315,13 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
                   const float* r, const float* rscale, const float* rshift, int relu,
                   float* y, float* y_stats, const float* gather_m, float* y_gathered, int B,
                   int C, int T, int V, void* stream);
+/* sgcn_bn_apply with folded finalizes: `fold` (per_joint == 0 only) supplies scale/shift,
+ * `rfold` (with r; rscale/rshift NULL) the residual's; either NULL = as sgcn_bn_apply. */
+int sgcn_bn_apply_fold(const float* x, const float* scale, const float* shift, int per_joint,
+                       const sgcn_bn_fold* fold, const float* r, const float* rscale,
+                       const float* rshift, const sgcn_bn_fold* rfold, int relu, float* y,
+                       float* y_stats, const float* gather_m, float* y_gathered, int B, int C,
+                       int T, int V, void* stream);
 
 /* Backward partials: g = dy * (relu ? y > 0 : 1); part[b][f] = {sum g, sum g*xhat};
  * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none).

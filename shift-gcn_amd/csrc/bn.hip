@@ -231,25 +231,15 @@ __global__ __launch_bounds__(64 * kFSW) void bn_finalize_kernel(
   double smean, sm2, smean2;
   int f;
   if (!feature_sums(part, B, F, smean, sm2, smean2, f)) return;
-  const double nb = (double)B, np_ = (double)n_part, n = nb * np_;
-  const double mean_d = smean / nb;
-  const double m2 = sm2 + np_ * (smean2 - smean * smean / nb);
-  const double var = n > 0 ? fmax(m2, 0.0) / n : 0.0;
-  const float mean = (float)mean_d;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const int rf = ref_feature(f, perm_V, F);
   const float g = gamma ? gamma[rf] : 1.f;
   const float bb = beta ? beta[rf] : 0.f;
-  const float scale = g * invstd;
-  mean_out[f] = mean;
-  invstd_out[f] = invstd;
-  scale_out[f] = scale;
-  shift_out[f] = bb - mean * scale;
-  if (running_mean) {
-    const double unbiased = n > 1 ? fmax(m2, 0.0) / (n - 1.0) : var;
-    running_mean[rf] = (1.f - momentum) * running_mean[rf] + momentum * mean;
-    running_var[rf] = (1.f - momentum) * running_var[rf] + momentum * (float)unbiased;
-  }
+  const BnCoef k = bn_train_coef(smean, sm2, smean2, B, n_part, eps, g, bb);
+  mean_out[f] = k.mean;
+  invstd_out[f] = k.invstd;
+  scale_out[f] = k.scale;
+  shift_out[f] = k.shift;
+  if (running_mean) bn_running_update(running_mean, running_var, rf, momentum, k);
 }
 
 // eval-mode coefficients from running statistics
@@ -391,7 +381,8 @@ __global__ __launch_bounds__(NT) void bn_apply_ja_kernel(
     const float* __restrict__ shift, const float* __restrict__ r,
     const float* __restrict__ rscale, const float* __restrict__ rshift,
     float* __restrict__ y, float2* __restrict__ ystats, const float* __restrict__ gm,
-    float* __restrict__ yg, int C, int T, int V) {
+    float* __restrict__ yg, int C, int T, int V, const sgcn_bn_fold fm = sgcn_bn_fold{},
+    const sgcn_bn_fold fr = sgcn_bn_fold{}) {
   constexpr bool OUT_STATS = OUTX == 1, OUT_G = OUTX == 2;
   __shared__ float red[2 * NT / 64];
   const int plane = blockIdx.x, c = plane % C, rc = c % V;
@@ -418,10 +409,28 @@ __global__ __launch_bounds__(NT) void bn_apply_ja_kernel(
       for (int e = 0; e < LPT; ++e) rv[e] = bload(rr, vo + e * vstep, 0);
     }
   }
-  const float sc = PER_JOINT ? scale[c * V + w] : scale[c];
-  const float sh = PER_JOINT ? shift[c * V + w] : shift[c];
+  // folded finalizes (sgcn_bn_fold, uniform per launch): the per-channel coefficients are
+  // merged from the batch partials here, while the plane's loads are in flight
+  float sc, sh;
+  if (!PER_JOINT && fm.part) {
+    const float2 k = bn_fold_channel(fm, c, C, plane / C, (int)gridDim.x / C);
+    sc = k.x;
+    sh = k.y;
+  } else {
+    sc = PER_JOINT ? scale[c * V + w] : scale[c];
+    sh = PER_JOINT ? shift[c * V + w] : shift[c];
+  }
   float rsc = 1.f, rsh = 0.f;
-  if (RES == 2) { rsc = rscale[c]; rsh = rshift[c]; }
+  if (RES == 2) {
+    if (fr.part) {
+      const float2 k = bn_fold_channel(fr, c, C, plane / C, (int)gridDim.x / C);
+      rsc = k.x;
+      rsh = k.y;
+    } else {
+      rsc = rscale[c];
+      rsh = rshift[c];
+    }
+  }
   const float gmu = OUT_G ? gm[wz * C + c] : 0.f;
   const auto yr = make_rsrc(y + off, pb);
   const auto ygr = make_rsrc(OUT_G ? yg + off : y + off, OUT_G ? pb : 0u);
@@ -1193,12 +1202,39 @@ int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
   return 0;
 }
 
+static int fold_check(const sgcn_bn_fold* f) {
+  SGCN_REQUIRE(!f || (f->part && f->n_part > 0 && f->mean && f->invstd && f->scale &&
+                      f->shift && (f->running_mean == nullptr) == (f->running_var == nullptr)));
+  return 0;
+}
+
+// the finalize of a fold as its own launch (consumers that do not fold)
+static int fold_resolve(const sgcn_bn_fold* f, int B, int C, void* stream) {
+  return sgcn_bn_finalize((const float*)f->part, B, C, f->n_part, 0, f->gamma, f->beta, f->eps,
+                          f->momentum, f->running_mean, f->running_var, f->num_batches,
+                          f->mean, f->invstd, f->scale, f->shift, stream);
+}
+
 int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
                   const float* r, const float* rscale, const float* rshift, int relu,
                   float* y, float* y_stats, const float* gather_m, float* y_gathered, int B,
                   int C, int T, int V, void* stream) {
+  return sgcn_bn_apply_fold(x, scale, shift, per_joint, nullptr, r, rscale, rshift, nullptr,
+                            relu, y, y_stats, gather_m, y_gathered, B, C, T, V, stream);
+}
+
+int sgcn_bn_apply_fold(const float* x, const float* scale, const float* shift, int per_joint,
+                       const sgcn_bn_fold* fold, const float* r, const float* rscale,
+                       const float* rshift, const sgcn_bn_fold* rfold, int relu, float* y,
+                       float* y_stats, const float* gather_m, float* y_gathered, int B, int C,
+                       int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
+  if (fold_check(fold) || fold_check(rfold)) return SGCN_EINVAL;
+  SGCN_REQUIRE(!fold || per_joint == 0);
+  SGCN_REQUIRE(!rfold || (r && !rscale && !rshift));
+  if (fold) { scale = fold->scale; shift = fold->shift; }
+  if (rfold) { rscale = rfold->scale; rshift = rfold->shift; }
   SGCN_REQUIRE(x && scale && shift && y);
   SGCN_REQUIRE((gather_m == nullptr) == (y_gathered == nullptr));
   SGCN_REQUIRE(!(y_stats && y_gathered) && y_gathered != y);
@@ -1214,9 +1250,10 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
       const int ox = ys ? 1 : (y_gathered ? 2 : 0);
+      const sgcn_bn_fold fm = fold ? *fold : sgcn_bn_fold{}, fr = rfold ? *rfold : sgcn_bn_fold{};
 #define SGCN_AJ(NT, L, PJ, RS, RL, OX, ZU)                                                     \
   bn_apply_ja_kernel<NT, L, PJ, RS, RL, OX, ZU><<<g, NT, 0, st>>>(                             \
-      x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V)
+      x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V, fm, fr)
 #define SGCN_AJ_L(NT, PJ, RS, RL, OX, ZU)                                                      \
   do {                                                                                         \
     if (lpt == 8) SGCN_AJ(NT, 8, PJ, RS, RL, OX, ZU);                                          \
@@ -1262,6 +1299,9 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
       return 0;
     }
   }
+  // the looping kernel reads finished coefficients: the folds' finalizes launch first
+  if (fold) { const int rc = fold_resolve(fold, B, C, stream); if (rc) return rc; }
+  if (rfold) { const int rc = fold_resolve(rfold, B, C, stream); if (rc) return rc; }
 #define SGCN_APPLY_X(PJ, RS, RL, OX)                                                        \
   bn_apply_kernel<PJ, RS, RL, OX><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale, rshift, y, \
                                                           ys, gather_m, y_gathered, C, T, V)

@@ -156,4 +156,92 @@ __host__ __device__ inline Moments merge(Moments a, Moments b) {
   return {n, a.mean + d * (b.n / n), a.m2 + b.m2 + d * d * (a.n * b.n / n)};
 }
 
+// Training-mode BatchNorm coefficients from the batch sums of per-plane {mean, M2}
+// partials (all B partials over n_part elements each): smean = sum mean_b, sm2 = sum M2_b,
+// smean2 = sum mean_b^2, in double. Shared by bn_finalize_kernel and the folded finalize
+// (bn_fold_channel), so both compute bit-identical values.
+struct BnCoef {
+  float mean, invstd, scale, shift;
+  double unbiased;
+};
+__device__ __forceinline__ BnCoef bn_train_coef(double smean, double sm2, double smean2, int B,
+                                                int n_part, float eps, float g, float bb) {
+  const double nb = (double)B, np_ = (double)n_part, n = nb * np_;
+  const double mean_d = smean / nb;
+  const double m2 = sm2 + np_ * (smean2 - smean * smean / nb);
+  const double var = n > 0 ? fmax(m2, 0.0) / n : 0.0;
+  BnCoef r;
+  r.mean = (float)mean_d;
+  r.invstd = (float)(1.0 / sqrt(var + (double)eps));
+  r.scale = g * r.invstd;
+  r.shift = bb - r.mean * r.scale;
+  r.unbiased = n > 1 ? fmax(m2, 0.0) / (n - 1.0) : var;
+  return r;
+}
+__device__ __forceinline__ void bn_running_update(float* rm, float* rv, int rf, float momentum,
+                                                  const BnCoef& c) {
+  rm[rf] = (1.f - momentum) * rm[rf] + momentum * c.mean;
+  rv[rf] = (1.f - momentum) * rv[rf] + momentum * (float)c.unbiased;
+}
+
+// The folded per-channel finalize (sgcn_bn_fold): returns channel c's (scale, shift) to
+// every thread of the workgroup (call from all threads: two barriers); the workgroup of
+// sample 0 also writes the statistics and the running-stat update. The batch sums follow
+// bn_finalize_kernel's order: sample b into partial sum (b mod 8), in increasing b, then the
+// eight merged 0..7 (feature_sums).
+__device__ __forceinline__ float2 bn_fold_channel(const sgcn_bn_fold& f, int c, int C, int b,
+                                                  int B) {
+  __shared__ double fs[8][3];
+  __shared__ float2 fr;
+  const int t = threadIdx.x;
+  const float2* __restrict__ part = (const float2*)f.part;
+  if (t < 8) {
+    double ax = 0.0, ay = 0.0, axx = 0.0;
+    int bb = t;
+    for (; bb + 24 < B; bb += 32) {   // 4 samples' loads in flight
+      float2 pv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pv[u] = part[(size_t)(bb + 8 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ax += pv[u].x;
+        ay += pv[u].y;
+        axx += (double)pv[u].x * pv[u].x;
+      }
+    }
+    for (; bb < B; bb += 8) {
+      const float2 pv = part[(size_t)bb * C + c];
+      ax += pv.x;
+      ay += pv.y;
+      axx += (double)pv.x * pv.x;
+    }
+    fs[t][0] = ax;
+    fs[t][1] = ay;
+    fs[t][2] = axx;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double ax = fs[0][0], ay = fs[0][1], axx = fs[0][2];
+    for (int q = 1; q < 8; ++q) {
+      ax += fs[q][0];
+      ay += fs[q][1];
+      axx += fs[q][2];
+    }
+    const float g = f.gamma ? f.gamma[c] : 1.f;
+    const float be = f.beta ? f.beta[c] : 0.f;
+    const BnCoef k = bn_train_coef(ax, ay, axx, B, f.n_part, f.eps, g, be);
+    fr = make_float2(k.scale, k.shift);
+    if (b == 0) {
+      f.mean[c] = k.mean;
+      f.invstd[c] = k.invstd;
+      f.scale[c] = k.scale;
+      f.shift[c] = k.shift;
+      if (f.running_mean) bn_running_update(f.running_mean, f.running_var, c, f.momentum, k);
+      if (c == 0 && f.num_batches) *f.num_batches += 1;
+    }
+  }
+  __syncthreads();
+  return fr;
+}
+
 }  // namespace sgcn

@@ -457,7 +457,8 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     int Ho, int stride, int add_half, const float* __restrict__ zs = nullptr,
     const float* __restrict__ zt = nullptr, const float* __restrict__ r = nullptr,
     const float* __restrict__ rs = nullptr, const float* __restrict__ rt = nullptr,
-    const float* __restrict__ gm = nullptr, float* __restrict__ og = nullptr) {
+    const float* __restrict__ gm = nullptr, float* __restrict__ og = nullptr,
+    const sgcn_bn_fold fa = sgcn_bn_fold{}) {
   static_assert(MODE != 1 || (AFFINE && RES >= 1 && !STATS), "pre: affine taps of relu(...)");
   static_assert(MODE != 2 || (!AFFINE && !STATS), "tail: plain taps");
   extern __shared__ float pl[];   // padded Hb x W input plane (affine applied) + 1 spare
@@ -471,7 +472,8 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
   const int nb = Hb * W, n = Ho * W;
   const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
   float a = 1.f, b = 0.f;
-  if (AFFINE) { a = scale[c]; b = shift[c]; }
+  const bool fold = MODE == 0 && AFFINE && fa.part != nullptr;   // uniform
+  if (AFFINE && !fold) { a = scale[c]; b = shift[c]; }
   float q1 = 1.f, q2 = 0.f;   // residual BatchNorm (RES 2)
   if (RES == 2) { q1 = rs[c]; q2 = rt[c]; }
   {
@@ -479,6 +481,11 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     float t[LPT], u[MODE == 1 ? LPT : 1];
 #pragma unroll
     for (int e = 0; e < LPT; ++e) t[e] = bload(ir, vo + e * vstep, 0);
+    if (fold) {   // the BatchNorm finalize of the input, while the plane's loads fly
+      const float2 ab = bn_fold_channel(fa, c, C, plane / C, (int)gridDim.x / C);
+      a = ab.x;
+      b = ab.y;
+    }
     if (MODE == 1) {
       const auto rr = make_rsrc(r + (size_t)plane * nb, (unsigned)nb * 4u);
 #pragma unroll
@@ -1288,13 +1295,15 @@ template <int NT>
 bool launch_fwd_pad(bool affine, bool stats, const float* in, float* out, const float* xpos,
                     const float* ypos, const float* scale, const float* shift, float2* ps,
                     int B, int C, int H, int W, int Ho, int stride, int add_half,
-                    hipStream_t st) {
+                    hipStream_t st, const sgcn_bn_fold* fold = nullptr) {
   const int lpt = pad_fwd_lpt(H, W, NT);
   const size_t lds = (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float);
   if (lpt == 0) return false;
+  const sgcn_bn_fold fa = fold ? *fold : sgcn_bn_fold{};
 #define SGCN_FWDP(L, A, S)                                                                   \
-  tshift_fwd_pad_kernel<NT, L, 0, A, S><<<B * C, NT, lds, st>>>(in, out, xpos, ypos, scale, shift, \
-                                                              ps, C, H, W, Ho, stride, add_half)
+  tshift_fwd_pad_kernel<NT, L, 0, A, S><<<B * C, NT, lds, st>>>(                             \
+      in, out, xpos, ypos, scale, shift, ps, C, H, W, Ho, stride, add_half, nullptr, nullptr, \
+      nullptr, nullptr, nullptr, nullptr, nullptr, fa)
 #define SGCN_FWDP_AS(L)                                                                      \
   do {                                                                                       \
     if (affine) { if (stats) SGCN_FWDP(L, true, true); else SGCN_FWDP(L, true, false); }     \
@@ -1468,6 +1477,40 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
   }
   SGCN_LAUNCH_CHECK();
   return 0;
+}
+
+int sgcn_tshift_fwd_fold(const float* in, float* out, const float* xpos, const float* ypos,
+                         const sgcn_bn_fold* fold, float* plane_stats, int B, int C, int H,
+                         int W, int stride, int ypos_is_raw, void* stream) {
+  if (!fold)
+    return sgcn_tshift_fwd(in, out, xpos, ypos, nullptr, nullptr, plane_stats, B, C, H, W,
+                           stride, ypos_is_raw, stream);
+  SGCN_REQUIRE(B >= 0 && C > 0 && H >= 0 && W > 0 && stride >= 1);
+  SGCN_REQUIRE(fold->part && fold->n_part > 0 && fold->mean && fold->invstd && fold->scale &&
+               fold->shift && (fold->running_mean == nullptr) == (fold->running_var == nullptr));
+  const int Ho = H / stride;
+  if (B == 0 || Ho == 0) return 0;
+  SGCN_REQUIRE(in && out && xpos && ypos);
+  SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  const bool stats = plane_stats != nullptr;
+  float2* ps = (float2*)plane_stats;
+  const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
+  if (H * W <= kFwdLdsMax2 &&
+      (H * W <= kFwdLdsMax
+           ? launch_fwd_pad<kThreads>(true, stats, in, out, xpos, ypos, fold->scale, fold->shift, ps, B, C, H, W, Ho, stride, ah, st, fold)
+           : launch_fwd_pad<512>(true, stats, in, out, xpos, ypos, fold->scale, fold->shift, ps, B, C, H, W, Ho, stride, ah, st, fold))) {
+    SGCN_LAUNCH_CHECK();
+    return 0;
+  }
+  // planes the padded kernel does not take: the finalize as its own launch
+  const int rc = sgcn_bn_finalize((const float*)fold->part, B, C, fold->n_part, 0, fold->gamma,
+                                  fold->beta, fold->eps, fold->momentum, fold->running_mean,
+                                  fold->running_var, fold->num_batches, fold->mean,
+                                  fold->invstd, fold->scale, fold->shift, stream);
+  if (rc) return rc;
+  return sgcn_tshift_fwd(in, out, xpos, ypos, fold->scale, fold->shift, plane_stats, B, C, H,
+                         W, stride, ypos_is_raw, stream);
 }
 
 int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const float* ypos,

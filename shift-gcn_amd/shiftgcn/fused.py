@@ -195,8 +195,8 @@ def gcn_forward(mod, x0, training, off=False):
         down = _OffPath(off, x0)
         with down:
             ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
-            if training:
-                dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn)
+            if training:   # (folded into the gcn tail's apply below)
+                dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn, defer=True)
             else:
                 dst = ops.bn_eval_coef(bn, Cout)
     cache = mod.__dict__.pop("_gather_cache", None)
@@ -408,7 +408,8 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
     if training:
         if h_moments is None:
             h_moments = ops.moments(H, False)
-        ast = ops.bn_finalize(h_moments, B, C, T * V, mod.bn)
+        # folded into the shift_in launch (sgcn_tshift_fwd_fold)
+        ast = ops.bn_finalize(h_moments, B, C, T * V, mod.bn, defer=True)
     else:
         ast = ops.bn_eval_coef(mod.bn, C)
     R = _empty(B, Cout, T, V, like=src)
@@ -430,8 +431,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
         ops.pw_fwd_tshift(tl.weight, tl.bias, PV(H), si.xpos.detach(), si.ypos.detach(), ast,
                           PV(R), Cout, C, T, V, relu=True, x_shifted=As)
     else:
-        As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride,
-                            scale=ast.scale, shift=ast.shift)
+        As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride, affine=ast)
         ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
     To = T // stride
     if tail is not None:
@@ -441,8 +441,8 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
                                    r=tail[0], rst=tail[1], gather_m=tail[2])
     stats = _empty(B * Cout * 2, like=src) if training else None
     S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
-    if training:
-        sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2)
+    if training:   # folded into the unit tail's apply
+        sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2, defer=True)
     else:
         sst = ops.bn_eval_coef(mod.bn2, Cout)
     s = TcnSaved()
@@ -519,8 +519,8 @@ def convbn_core_forward(mod, x, training):
     To = (T - 1) // s_t + 1
     Rc = _empty(B, Cout, To, V, like=x)
     ops.pw_fwd(conv.weight, False, conv.bias, PV(x, s_t), PV(Rc), Cout, Cin, To, V)
-    if training:
-        rst = ops.bn_finalize(ops.moments(Rc, False), B, Cout, To * V, bn)
+    if training:   # folded into the unit tail's apply
+        rst = ops.bn_finalize(ops.moments(Rc, False), B, Cout, To * V, bn, defer=True)
     else:
         rst = ops.bn_eval_coef(bn, Cout)
     s = ConvBnSaved()

@@ -7,6 +7,8 @@ enqueues on torch's CURRENT stream (so hipGraph capture and multi-stream use wor
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -167,11 +169,19 @@ def _opt(t, name):
 # temporal shift
 # --------------------------------------------------------------------------------------
 def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=None,
-               ypos_is_raw=True):
+               ypos_is_raw=True, affine=None):
     """Forward shift of ``inp`` (B,C,H,W) -> (B,C,H//stride,W). ``ypos`` is the RAW
     parameter (the +0.5 for stride != 1 is applied in-kernel). Optional fused
-    per-channel input affine (scale, shift) and per-plane output moments ``stats``
-    (B*C*2 floats). float64 tensors run the double-precision kernel (no fused options)."""
+    per-channel input affine (scale, shift) — or ``affine``, a BnStats whose pending
+    finalize the shift folds (sgcn_tshift_fwd_fold) — and per-plane output moments
+    ``stats`` (B*C*2 floats). float64 tensors run the double-precision kernel (no fused
+    options)."""
+    if affine is not None:
+        fold = affine.take_fold()
+        if fold is None:
+            scale, shift = affine.scale, affine.shift
+        else:
+            return _tshift_fwd_fold(inp, xpos, ypos, stride, fold, stats, out, ypos_is_raw)
     if inp.dtype == torch.float64:
         if scale is not None or shift is not None or stats is not None:
             raise RuntimeError("the fused shift options are float32-only")
@@ -190,6 +200,24 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
                                  _ptr(shift), _ptr(stats), B, C, H, W, stride,
                                  int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_fwd")
+    return out
+
+
+def _tshift_fwd_fold(inp, xpos, ypos, stride, fold, stats, out, ypos_is_raw):
+    check_input(inp, "input")
+    check_input(xpos, "xpos")
+    check_input(ypos, "ypos")
+    _opt(stats, "stats")
+    B, C, H, W = inp.shape
+    if out is None:
+        out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
+    f, _keep = fold
+    nb = 4 * (inp.numel() + out.numel())
+    with _timed("tshift_fwd", 0, nb, inp, "FOLD " + _shp(inp)):
+        rc = _lib.load().sgcn_tshift_fwd_fold(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos),
+                                              ctypes.byref(f), _ptr(stats), B, C, H, W, stride,
+                                              int(ypos_is_raw), _stream(inp))
+    _lib.check(rc, "sgcn_tshift_fwd_fold")
     return out
 
 
@@ -606,35 +634,125 @@ def moments(x, per_joint):
     return part
 
 
+class BnFoldStruct(ctypes.Structure):
+    """``sgcn_bn_fold`` (include/shiftgcn.h): a training BatchNorm finalize folded into its
+    first consumer's prologue."""
+    _fields_ = [("part", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
+                ("beta", ctypes.c_void_p), ("running_mean", ctypes.c_void_p),
+                ("running_var", ctypes.c_void_p), ("num_batches", ctypes.c_void_p),
+                ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
+                ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p),
+                ("n_part", ctypes.c_int), ("eps", ctypes.c_float),
+                ("momentum", ctypes.c_float)]
+
+
 class BnStats:
     """Statistics and apply coefficients of one BatchNorm call (local feature order):
-    batch statistics in training mode, running statistics in eval mode (``batch``)."""
+    batch statistics in training mode, running statistics in eval mode (``batch``).
 
-    __slots__ = ("mean", "invstd", "scale", "shift", "batch")
+    A training-mode per-channel finalize may be left PENDING (``bn_finalize(...,
+    defer=True)``, round 4): a consumer that folds it (sgcn_tshift_fwd_fold,
+    sgcn_bn_apply_fold) takes it with :meth:`take_fold` and its plane workgroups compute the
+    coefficients; anything else that reads ``mean``/``invstd``/``scale``/``shift`` first
+    launches the finalize (:meth:`resolve`), on the current stream."""
+
+    __slots__ = ("_mean", "_invstd", "_scale", "_shift", "_buf", "batch", "_pending")
 
     def __init__(self, F, device, batch=True):
         buf = torch.empty((4, F), device=device, dtype=_F32)
-        self.mean, self.invstd, self.scale, self.shift = buf[0], buf[1], buf[2], buf[3]
+        self._buf = buf
+        self._mean, self._invstd, self._scale, self._shift = buf[0], buf[1], buf[2], buf[3]
         self.batch = batch
+        self._pending = None
+
+    @property
+    def mean(self):
+        self.resolve()
+        return self._mean
+
+    @property
+    def invstd(self):
+        self.resolve()
+        return self._invstd
+
+    @property
+    def scale(self):
+        self.resolve()
+        return self._scale
+
+    @property
+    def shift(self):
+        self.resolve()
+        return self._shift
+
+    @property
+    def pending(self):
+        return self._pending is not None
+
+    def resolve(self):
+        """Launch the pending finalize (sgcn_bn_finalize), if any."""
+        p, self._pending = self._pending, None
+        if p is None:
+            return
+        part, B, F, n_part, bn, track = p
+        momentum = bn.momentum if bn.momentum is not None else 0.0
+        part.record_stream(torch.cuda.current_stream(part.device))
+        with _timed("finalize", 0, 4 * part.numel(), part):
+            rc = _lib.load().sgcn_bn_finalize(
+                _ptr(part), B, F, n_part, 0, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps),
+                float(momentum), _ptr(bn.running_mean) if track else None,
+                _ptr(bn.running_var) if track else None,
+                _ptr(bn.num_batches_tracked) if track else None, _ptr(self._mean),
+                _ptr(self._invstd), _ptr(self._scale), _ptr(self._shift), _stream(part))
+        _lib.check(rc, "sgcn_bn_finalize")
+
+    def take_fold(self):
+        """(ctypes struct, keep-alive) of the pending finalize for a folding consumer, which
+        then writes the statistics; None if nothing is pending."""
+        p, self._pending = self._pending, None
+        if p is None:
+            return None
+        part, B, F, n_part, bn, track = p
+        cur = torch.cuda.current_stream(part.device)
+        part.record_stream(cur)          # made (or allocated) on another stream
+        self._buf.record_stream(cur)
+        momentum = bn.momentum if bn.momentum is not None else 0.0
+        f = BnFoldStruct(_ptr(part), _ptr(bn.weight), _ptr(bn.bias),
+                         _ptr(bn.running_mean) if track else None,
+                         _ptr(bn.running_var) if track else None,
+                         _ptr(bn.num_batches_tracked) if track else None, _ptr(self._mean),
+                         _ptr(self._invstd), _ptr(self._scale), _ptr(self._shift),
+                         int(n_part), float(bn.eps), float(momentum))
+        return f, part
 
 
-def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
+# Per-channel training finalizes left pending for their consumer to fold (round 4;
+# SGCN_FOLD_FINALIZE=0: every finalize its own launch, A/B knob)
+FOLD_FINALIZE = int(__import__("os").environ.get("SGCN_FOLD_FINALIZE", "1"))
+
+
+def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True, defer=False):
     """Training-mode statistics of ``bn`` (an nn.BatchNorm*d) from partials; updates its
-    running stats / num_batches_tracked exactly once, like ``bn.forward`` in train()."""
+    running stats / num_batches_tracked exactly once, like ``bn.forward`` in train().
+    ``defer`` (per-channel only): leave the finalize pending in the returned BnStats for a
+    consumer to fold (BnStats.take_fold), or launched on first read."""
     st = BnStats(F, part.device)
     lib = _lib.load()
     track = training and bn.track_running_stats and bn.running_mean is not None
     if track and bn.momentum is None:
         # the cumulative moving average (momentum=None) is never used by the reference
         raise NotImplementedError("BatchNorm momentum=None is not supported on the HIP path")
+    if defer and FOLD_FINALIZE and perm_V == 0:
+        st._pending = (part, B, F, n_part, bn, track)
+        return st
     momentum = bn.momentum if bn.momentum is not None else 0.0
     with _timed("finalize", 0, 4 * part.numel(), part):
         rc = lib.sgcn_bn_finalize(
             _ptr(part), B, F, n_part, perm_V, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps),
             float(momentum), _ptr(bn.running_mean) if track else None,
             _ptr(bn.running_var) if track else None,
-            _ptr(bn.num_batches_tracked) if track else None, _ptr(st.mean), _ptr(st.invstd),
-            _ptr(st.scale), _ptr(st.shift), _stream(part))
+            _ptr(bn.num_batches_tracked) if track else None, _ptr(st._mean),
+            _ptr(st._invstd), _ptr(st._scale), _ptr(st._shift), _stream(part))
     _lib.check(rc, "sgcn_bn_finalize")
     return st
 
@@ -663,14 +781,20 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
     ys = torch.empty((B * C * 2,), device=x.device, dtype=_F32) if out_stats else None
     yg = torch.empty_like(y) if gather_m is not None else None
     nb = 4 * x.numel() * (2 + (r is not None) + (yg is not None))
-    with _timed("bn_apply", 0, nb, x, _shp(x)):
-        rc = _lib.load().sgcn_bn_apply(_ptr(x), _ptr(st.scale), _ptr(st.shift),
-                                       int(per_joint), _ptr(r),
-                                       _ptr(rst.scale) if rst else None,
-                                       _ptr(rst.shift) if rst else None, int(relu), _ptr(y),
-                                       _ptr(ys), _ptr(gather_m), _ptr(yg), B, C, T, V,
-                                       _stream(x))
-    _lib.check(rc, "sgcn_bn_apply")
+    # pending per-channel finalizes are folded into this launch (sgcn_bn_apply_fold)
+    fm = st.take_fold() if (not per_joint and st.pending) else None
+    fr = rst.take_fold() if (rst is not None and rst.pending) else None
+    sc = st._scale if fm is not None else st.scale
+    sh = st._shift if fm is not None else st.shift
+    with _timed("bn_apply", 0, nb, x, ("FOLD " if fm or fr else "") + _shp(x)):
+        rc = _lib.load().sgcn_bn_apply_fold(
+            _ptr(x), _ptr(sc), _ptr(sh), int(per_joint),
+            ctypes.byref(fm[0]) if fm is not None else None, _ptr(r),
+            _ptr(rst.scale) if (rst is not None and fr is None) else None,
+            _ptr(rst.shift) if (rst is not None and fr is None) else None,
+            ctypes.byref(fr[0]) if fr is not None else None, int(relu), _ptr(y), _ptr(ys),
+            _ptr(gather_m), _ptr(yg), B, C, T, V, _stream(x))
+    _lib.check(rc, "sgcn_bn_apply_fold")
     if gather_m is not None:
         return y, yg
     return y if out_stats is None else (y, ys)
