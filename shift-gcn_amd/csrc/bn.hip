@@ -674,7 +674,14 @@ __global__ __launch_bounds__(64 * kFSW) void bn_bwd_finalize_kernel(
 // kGbnW waves take every kGbnW-th sample (4 rows in flight), merged in fixed order
 // through LDS. (The one-wave-per-feature form with lanes striding the batch cost a cache
 // line per lane and load: 19 us average per call at F = 1,600-6,400, B = 128.)
-constexpr int kGbnW = 16;
+// Waves per workgroup: this launch is on the critical path while the side stream's
+// weight-gradient contractions hold most CUs; a 1,024-thread workgroup (16 waves, 46 KB of
+// LDS) waits for a whole CU to drain (92 us per call in the overlapped trace,
+// profiles/r04_gbnfin/), smaller ones fit in beside them.
+#ifndef SGCN_GBN_WAVES
+#define SGCN_GBN_WAVES 4
+#endif
+constexpr int kGbnW = SGCN_GBN_WAVES;
 __global__ __launch_bounds__(64 * kGbnW) void bn_bwd_finalize_gbn_kernel(
     const float* __restrict__ part6, int B, int F, int V, double n_total,
     const float* __restrict__ dyc, const float* __restrict__ dym, int C,
