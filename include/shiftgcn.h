@@ -38,6 +38,48 @@ extern "C" {
  * sgcn_pw_fwd_bn_res (the inference Shift_gcn tail in the contraction epilogue). */
 int sgcn_abi_version(void);
 
+/* A training-mode per-channel BatchNorm finalize FOLDED into its first consumer (round 4):
+ * the consumer's (sample, channel) plane workgroups each merge their channel's B partials
+ * (sgcn_moments / sgcn_tshift_fwd plane_stats layout, (B*C) float2 {mean, M2} over n_part
+ * elements each) in sgcn_bn_finalize's order, so the coefficients are bit-identical to
+ * that kernel's; the workgroup of sample 0 writes mean/invstd/scale/shift (C each) and
+ * updates the running statistics (gamma/beta NULL = 1/0; running_* NULL = not tracked;
+ * num_batches += 1 once). Consumers: sgcn_tshift_fwd_fold, sgcn_bn_apply_fold. */
+typedef struct sgcn_bn_fold {
+  const void* part;
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  long long* num_batches;
+  float* mean;
+  float* invstd;
+  float* scale;
+  float* shift;
+  int n_part;
+  float eps;
+  float momentum;
+} sgcn_bn_fold;
+
+/* A per-channel BatchNorm BACKWARD finalize folded into its consumer (round 4): the
+ * consumer's plane workgroups merge part ((B*C) float2 {sum g, sum g*xhat}, the
+ * sgcn_bn_bwd_reduce / sgcn_gcn_dx_finish / sgcn_tshift_bwd bn_part layout) in
+ * sgcn_bn_bwd_finalize's order into that kernel's coefficients; the workgroup of sample 0
+ * writes coef[3][C] and dgamma/dbeta (NULL = not written; accumulate 0). mean/invstd: the
+ * BatchNorm's forward statistics; batch_stats 0 = a running-statistics BatchNorm.
+ * Consumers: sgcn_tshift_bwd_bnin_fold, sgcn_bn_bwd_apply_fold. */
+typedef struct sgcn_bn_bwd_fold {
+  const void* part;
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+  double n_total;
+  int batch_stats;
+} sgcn_bn_bwd_fold;
+
 /* ------------------------------------------------------------------------------------
  * Temporal shift
  * ------------------------------------------------------------------------------------ */
@@ -97,6 +139,13 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
                          const float* in, const float* xpos, const float* ypos, float* gin,
                          float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                          int W, int ypos_is_raw, void* stream);
+/* sgcn_tshift_bwd_bnin with bn2's backward finalize folded in (`fold`, coef NULL; fold->coef
+ * is written). Same plane limits. */
+int sgcn_tshift_bwd_bnin_fold(const float* dy, const float* y, const float* s,
+                              const float* coef, const sgcn_bn_bwd_fold* fold, const float* in,
+                              const float* xpos, const float* ypos, float* gin, float* gx,
+                              float* gy, void* ws, size_t ws_bytes, int B, int C, int H, int W,
+                              int ypos_is_raw, void* stream);
 
 /* Workspace bytes for sgcn_tshift_bwd (B*C float2 plane partials). */
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
@@ -264,28 +313,6 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
  * mean, invstd, scale = gamma*invstd, shift = beta - mean*scale (all [F], local feature
  * order); updates running_mean/var (momentum, unbiased var) and num_batches (+1) when
  * non-NULL, in the reference feature order (perm_V > 0: per-joint mapping). */
-/* A training-mode per-channel BatchNorm finalize FOLDED into its first consumer (round 4):
- * the consumer's (sample, channel) plane workgroups each merge their channel's B partials
- * (sgcn_moments / sgcn_tshift_fwd plane_stats layout, (B*C) float2 {mean, M2} over n_part
- * elements each) in sgcn_bn_finalize's order, so the coefficients are bit-identical to
- * that kernel's; the workgroup of sample 0 writes mean/invstd/scale/shift (C each) and
- * updates the running statistics (gamma/beta NULL = 1/0; running_* NULL = not tracked;
- * num_batches += 1 once). Consumers: sgcn_tshift_fwd_fold, sgcn_bn_apply_fold. */
-typedef struct sgcn_bn_fold {
-  const void* part;
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  long long* num_batches;
-  float* mean;
-  float* invstd;
-  float* scale;
-  float* shift;
-  int n_part;
-  float eps;
-  float momentum;
-} sgcn_bn_fold;
 
 /* sgcn_tshift_fwd with the input affine (in_scale/in_shift) of a folded finalize: `fold`
  * (NULL = no affine) writes fold->mean/invstd/scale/shift (C). Planes the padded LDS
@@ -293,6 +320,7 @@ typedef struct sgcn_bn_fold {
 int sgcn_tshift_fwd_fold(const float* in, float* out, const float* xpos, const float* ypos,
                          const sgcn_bn_fold* fold, float* plane_stats, int B, int C, int H,
                          int W, int stride, int ypos_is_raw, void* stream);
+
 
 int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
                      const float* gamma, const float* beta, float eps, float momentum,
@@ -358,6 +386,13 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
                       const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
                       void* stream);
+/* sgcn_bn_bwd_apply with folded backward finalizes: `fold` (per_joint 0; coef ignored) and
+ * `rfold` (with r and dr; rcoef NULL); either NULL = as sgcn_bn_bwd_apply. */
+int sgcn_bn_bwd_apply_fold(const float* dy, const float* y, int relu, const float* x,
+                           const float* coef, int per_joint, const sgcn_bn_bwd_fold* fold,
+                           const float* r, const float* rcoef, const sgcn_bn_bwd_fold* rfold,
+                           const float* dy_coef, float* dx, float* dr, int B, int C, int T,
+                           int V, void* stream);
 
 /* m = tanh(Feature_Mask) + 1 (shift_gcn.py:129); n = V*C. */
 int sgcn_mask_prep(const float* mask, float* m, int n, void* stream);

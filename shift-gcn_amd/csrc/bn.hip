@@ -654,15 +654,10 @@ __global__ __launch_bounds__(64 * kFSW) void bn_bwd_finalize_kernel(
   if (dgamma) dgamma[rf] = accumulate ? dgamma[rf] + (float)sgx : (float)sgx;
   if (dbeta) dbeta[rf] = accumulate ? dbeta[rf] + (float)sg : (float)sg;
   const float g = gamma ? gamma[rf] : 1.f;
-  const float is = invstd[f];
-  const float k1 = g * is;
-  // running-statistics (eval) BatchNorm is a fixed affine map: dx = k1 * g
-  const float k2 = batch_stats ? (float)(-(double)k1 * (double)is * (sgx / n_total)) : 0.f;
-  const float k3 = batch_stats ? (float)(-(double)k1 * (sg / n_total) - (double)k2 * (double)mean[f])
-                               : 0.f;
-  coef[f] = k1;
-  coef[F + f] = k2;
-  coef[2 * F + f] = k3;
+  const float3 k = bn_bwd_coef(sg, sgx, g, invstd[f], mean[f], n_total, batch_stats);
+  coef[f] = k.x;
+  coef[F + f] = k.y;
+  coef[2 * F + f] = k.z;
 }
 
 // The same from the k-free per-(plane, joint) sums of sgcn_tshift_bwd_gbn:
@@ -826,7 +821,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_ja_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ coef, int F, const float* __restrict__ r,
     const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
-    float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V) {
+    float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V,
+    const sgcn_bn_bwd_fold fm = sgcn_bn_bwd_fold{}, const sgcn_bn_bwd_fold fr = sgcn_bn_bwd_fold{}) {
   static_assert(PJM == 0 || PJM == 3, "per-channel, or per-joint gathered (ZU)");
   constexpr bool PER_JOINT = PJM == 3;
   const int plane = blockIdx.x, c = plane % C, rc = c % V;
@@ -861,10 +857,31 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_ja_kernel(
     }
   }
   const int f = PER_JOINT ? c * V + w : c;
-  const float k1 = coef[f], k2 = coef[F + f], k3 = coef[2 * F + f];
+  float k1, k2, k3;
+  if (!PER_JOINT && fm.part) {   // folded backward finalizes (uniform per launch)
+    const float3 k = bn_bwd_fold_channel(fm, c, C, plane / C, (int)gridDim.x / C);
+    k1 = k.x;
+    k2 = k.y;
+    k3 = k.z;
+  } else {
+    k1 = coef[f];
+    k2 = coef[F + f];
+    k3 = coef[2 * F + f];
+  }
   float d1 = 1.f, d2 = 0.f, d3 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
   if (DYT) { d1 = dyc[c]; d2 = dyc[C + c]; d3 = dyc[2 * C + c]; }
-  if (RES == 2) { q1 = rcoef[c]; q2 = rcoef[RF + c]; q3 = rcoef[2 * RF + c]; }
+  if (RES == 2) {
+    if (fr.part) {
+      const float3 k = bn_bwd_fold_channel(fr, c, C, plane / C, (int)gridDim.x / C);
+      q1 = k.x;
+      q2 = k.y;
+      q3 = k.z;
+    } else {
+      q1 = rcoef[c];
+      q2 = rcoef[RF + c];
+      q3 = rcoef[2 * RF + c];
+    }
+  }
   const auto dxr = make_rsrc(dx + off, pb);
   const auto drr = make_rsrc(RES ? dr + off : dx + off, RES ? pb : 0u);
 #pragma unroll
@@ -1423,12 +1440,37 @@ int sgcn_bn_bwd_finalize_gbn(const float* part6, int B, int C, int V, long long 
   return 0;
 }
 
+static int bwd_fold_check(const sgcn_bn_bwd_fold* f) {
+  SGCN_REQUIRE(!f || (f->part && f->mean && f->invstd && f->coef && f->n_total > 0));
+  return 0;
+}
+
+static int bwd_fold_resolve(const sgcn_bn_bwd_fold* f, int B, int C, void* stream) {
+  return sgcn_bn_bwd_finalize((const float*)f->part, B, C, (long long)f->n_total, 0, f->mean,
+                              f->invstd, f->gamma, f->dgamma, f->dbeta, 0, f->batch_stats,
+                              f->coef, stream);
+}
+
 int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
                       const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
                       void* stream) {
+  return sgcn_bn_bwd_apply_fold(dy, y, relu, x, coef, per_joint, nullptr, r, rcoef, nullptr,
+                                dy_coef, dx, dr, B, C, T, V, stream);
+}
+
+int sgcn_bn_bwd_apply_fold(const float* dy, const float* y, int relu, const float* x,
+                           const float* coef, int per_joint, const sgcn_bn_bwd_fold* fold,
+                           const float* r, const float* rcoef, const sgcn_bn_bwd_fold* rfold,
+                           const float* dy_coef, float* dx, float* dr, int B, int C, int T,
+                           int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
+  if (bwd_fold_check(fold) || bwd_fold_check(rfold)) return SGCN_EINVAL;
+  SGCN_REQUIRE(!fold || per_joint == 0);
+  SGCN_REQUIRE(!rfold || (r && dr && !rcoef));
+  if (fold) coef = fold->coef;
+  if (rfold) rcoef = rfold->coef;
   SGCN_REQUIRE(dy && x && coef && dx && (y || !relu));
   SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE(!rcoef || (r && dr));
@@ -1442,11 +1484,13 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
     const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
+      const sgcn_bn_bwd_fold fm = fold ? *fold : sgcn_bn_bwd_fold{};
+      const sgcn_bn_bwd_fold fr = rfold ? *rfold : sgcn_bn_bwd_fold{};
 #define SGCN_BJ(NT, L, PJ, RL, RS)                                                             \
   (dy_coef ? bn_bwd_apply_ja_kernel<NT, L, PJ, RL, RS, true><<<g, NT, 0, st>>>(                 \
-                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V)                     \
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V, fm, fr)             \
            : bn_bwd_apply_ja_kernel<NT, L, PJ, RL, RS, false><<<g, NT, 0, st>>>(                \
-                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V))
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V, fm, fr))
 #define SGCN_BJ_L(NT, PJ, RL, RS)                                                              \
   do {                                                                                         \
     if (lpt == 8) SGCN_BJ(NT, 8, PJ, RL, RS);                                                  \
@@ -1473,6 +1517,8 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
       return 0;
     }
   }
+  if (fold) { const int rc = bwd_fold_resolve(fold, B, C, stream); if (rc) return rc; }
+  if (rfold) { const int rc = bwd_fold_resolve(rfold, B, C, stream); if (rc) return rc; }
 #define SGCN_BA(PJ, RL, RS)                                                                   \
   (dy_coef ? bn_bwd_apply_kernel<PJ, RL, RS, true><<<g, kThreads, 0, st>>>(                      \
                  dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V)                      \

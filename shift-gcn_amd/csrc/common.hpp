@@ -244,4 +244,68 @@ __device__ __forceinline__ float2 bn_fold_channel(const sgcn_bn_fold& f, int c, 
   return fr;
 }
 
+// Training BatchNorm backward coefficients (dx = k1*g + k2*x + k3) from the batch sums
+// sg = sum g, sgx = sum g*xhat (bn_bwd_finalize_kernel's math; shared with the fold).
+__device__ __forceinline__ float3 bn_bwd_coef(double sg, double sgx, float g, float is,
+                                              float mean, double n_total, int batch_stats) {
+  const float k1 = g * is;
+  // running-statistics (eval) BatchNorm is a fixed affine map: dx = k1 * g
+  const float k2 = batch_stats ? (float)(-(double)k1 * (double)is * (sgx / n_total)) : 0.f;
+  const float k3 = batch_stats ? (float)(-(double)k1 * (sg / n_total) - (double)k2 * (double)mean)
+                               : 0.f;
+  return make_float3(k1, k2, k3);
+}
+
+// The folded backward finalize (sgcn_bn_bwd_fold): channel c's (k1, k2, k3) to every
+// thread (two barriers, call from all threads); sample 0's workgroup writes coef and
+// dgamma/dbeta. Sums in feature_sums order (see bn_fold_channel).
+__device__ __forceinline__ float3 bn_bwd_fold_channel(const sgcn_bn_bwd_fold& f, int c, int C,
+                                                      int b, int B) {
+  __shared__ double fs[8][2];
+  __shared__ float3 fr;
+  const int t = threadIdx.x;
+  const float2* __restrict__ part = (const float2*)f.part;
+  if (t < 8) {
+    double ax = 0.0, ay = 0.0;
+    int bb = t;
+    for (; bb + 24 < B; bb += 32) {
+      float2 pv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pv[u] = part[(size_t)(bb + 8 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ax += pv[u].x;
+        ay += pv[u].y;
+      }
+    }
+    for (; bb < B; bb += 8) {
+      const float2 pv = part[(size_t)bb * C + c];
+      ax += pv.x;
+      ay += pv.y;
+    }
+    fs[t][0] = ax;
+    fs[t][1] = ay;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double sg = fs[0][0], sgx = fs[0][1];
+    for (int q = 1; q < 8; ++q) {
+      sg += fs[q][0];
+      sgx += fs[q][1];
+    }
+    const float g = f.gamma ? f.gamma[c] : 1.f;
+    const float3 k = bn_bwd_coef(sg, sgx, g, f.invstd[c], f.mean[c], f.n_total, f.batch_stats);
+    fr = k;
+    if (b == 0) {
+      if (f.dgamma) f.dgamma[c] = (float)sgx;
+      if (f.dbeta) f.dbeta[c] = (float)sg;
+      f.coef[c] = k.x;
+      f.coef[C + c] = k.y;
+      f.coef[2 * C + c] = k.z;
+    }
+  }
+  __syncthreads();
+  return fr;
+}
+
 }  // namespace sgcn

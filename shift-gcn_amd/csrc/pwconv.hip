@@ -1162,13 +1162,19 @@ int dw3_splits(int M, int Nc, int P, int bkp, int tiles, int target) {
 struct Dw3Cfg {
   int bm, bn, bkp, target;
 };
+// positions per chunk of the 256-row weight-gradient tiles (A/B knob: 8 halves their LDS,
+// 74 -> 37 KB at 256 x 256, leaving room on the CU for the critical path's kernels while
+// the side stream runs them)
+#ifndef SGCN_DW3_BKP_BIG
+#define SGCN_DW3_BKP_BIG 16
+#endif
 Dw3Cfg dw3_cfg(int M, int Nc) {
   if (M <= 64 && Nc <= 64) return {64, 64, 32, 2048};
   if (M <= 128 && Nc <= 64) return {128, 64, 16, 1536};
   if (M <= 64 && Nc <= 128) return {64, 128, 16, 1536};
   if (M <= 128 && Nc <= 128) return {128, 128, 16, 1024};
-  if (Nc <= 128) return {256, 128, 16, 512};
-  return {256, 256, 16, 512};
+  if (Nc <= 128) return {256, 128, SGCN_DW3_BKP_BIG, 512};
+  return {256, 256, SGCN_DW3_BKP_BIG, 512};
 }
 
 template <int BM, int BN, int WM, int WN, int BKP>
@@ -1205,8 +1211,8 @@ int launch_dw3(const DwArgs& a0, hipStream_t st, float* ws, bool bias) {
   else if (c.bm == 128 && c.bn == 64) launch_dw3_t<128, 64, 2, 2, 16>(a, S, tiles, st);
   else if (c.bm == 64 && c.bn == 128) launch_dw3_t<64, 128, 2, 2, 16>(a, S, tiles, st);
   else if (c.bm == 128) launch_dw3_t<128, 128, 2, 2, 16>(a, S, tiles, st);
-  else if (c.bn == 128) launch_dw3_t<256, 128, 4, 2, 16>(a, S, tiles, st);
-  else launch_dw3_t<256, 256, 4, 2, 16>(a, S, tiles, st);
+  else if (c.bn == 128) launch_dw3_t<256, 128, 4, 2, SGCN_DW3_BKP_BIG>(a, S, tiles, st);
+  else launch_dw3_t<256, 256, 4, 2, SGCN_DW3_BKP_BIG>(a, S, tiles, st);
   return S;
 }
 

@@ -943,7 +943,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
     const float* __restrict__ gz, const float* __restrict__ gzm,
     const float* __restrict__ gzi, float* __restrict__ gzpart, const float* __restrict__ gd = nullptr,
     const float* __restrict__ gdm = nullptr, const float* __restrict__ gdi = nullptr,
-    float* __restrict__ gdpart = nullptr) {
+    float* __restrict__ gdpart = nullptr, const sgcn_bn_bwd_fold gf = sgcn_bn_bwd_fold{}) {
   static_assert(!GBN || (AFFINE && BNP && !GP), "GBN: shift_in with BNP");
   static_assert(!GBD || GBN, "GBD extends GBN");
   extern __shared__ float lds[];   // [(H + 2*kPadRows) * WP] padded gout (GBN: >= 6*NT)
@@ -975,7 +975,6 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
       const auto dyr = make_rsrc(gdy + poff, nbytes);
       const auto yr = make_rsrc(gy + poff, nbytes);
       const auto xr = make_rsrc(gx + poff, nbytes);
-      const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
       float u1[LPT], u2[LPT];
 #pragma unroll
       for (int e = 0; e < LPT; ++e) {
@@ -984,6 +983,19 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
         u1[e] = bload(yr, vb, 0);
         u2[e] = bload(xr, vb, 0);
         rin_r[e] = bload(inr, vb, 0);
+      }
+      // bn2's backward coefficients: read, or its backward finalize folded in (uniform),
+      // while the plane's loads fly
+      float k1, k2, k3;
+      if (gf.part) {
+        const float3 k = bn_bwd_fold_channel(gf, c, C, plane / C, (int)gridDim.x / C);
+        k1 = k.x;
+        k2 = k.y;
+        k3 = k.z;
+      } else {
+        k1 = gcoef[c];
+        k2 = gcoef[C + c];
+        k3 = gcoef[2 * C + c];
       }
 #pragma unroll
       for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
@@ -1406,14 +1418,16 @@ bool launch_ra(int nt, const float* gout, const float* in, const float* xpos,
                int W, const float* gdy, const float* gy, const float* gx, const float* gcoef,
                const float* gz, const float* gzm, const float* gzi, float* gzpart,
                hipStream_t st, const float* gd = nullptr, const float* gdm = nullptr,
-               const float* gdi = nullptr, float* gdpart = nullptr) {
+               const float* gdi = nullptr, float* gdpart = nullptr,
+               const sgcn_bn_bwd_fold* gfold = nullptr) {
   const int lpt = ra_lpt(H * W, nt, W);
   const size_t lds = ra_lds_bytes(H, W, nt, GBN);
   if (lpt == 0 || lds > kRaLdsMax) return false;
+  const sgcn_bn_bwd_fold gf = gfold ? *gfold : sgcn_bn_bwd_fold{};
 #define SGCN_RA(NT, L)                                                                         \
   tshift_bwd_ra_kernel<NT, L, AFFINE, RELU, BNP, GP, GBN, GBD><<<B * C, NT, lds, st>>>(        \
       gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, gdy, gy, gx, gcoef,  \
-      gz, gzm, gzi, gzpart, gd, gdm, gdi, gdpart)
+      gz, gzm, gzi, gzpart, gd, gdm, gdi, gdpart, gf)
   if (nt == 256) {
     if (lpt == 8) SGCN_RA(256, 8); else if (lpt == 16) SGCN_RA(256, 16); else if (lpt == 24) SGCN_RA(256, 24); else SGCN_RA(256, 32);
   } else {
@@ -1646,8 +1660,20 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
                          const float* in, const float* xpos, const float* ypos, float* gin,
                          float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                          int W, int ypos_is_raw, void* stream) {
+  return sgcn_tshift_bwd_bnin_fold(dy, y, s, coef, nullptr, in, xpos, ypos, gin, gx, gy, ws,
+                                   ws_bytes, B, C, H, W, ypos_is_raw, stream);
+}
+
+int sgcn_tshift_bwd_bnin_fold(const float* dy, const float* y, const float* s,
+                              const float* coef, const sgcn_bn_bwd_fold* fold, const float* in,
+                              const float* xpos, const float* ypos, float* gin, float* gx,
+                              float* gy, void* ws, size_t ws_bytes, int B, int C, int H, int W,
+                              int ypos_is_raw, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0);
   SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
+  SGCN_REQUIRE(!fold || (fold->part && fold->mean && fold->invstd && fold->coef &&
+                         fold->n_total > 0));
+  if (fold) coef = fold->coef;
   SGCN_REQUIRE(dy && y && s && coef && in && xpos && ypos && gin && ws);
   SGCN_REQUIRE((gx == nullptr) == (gy == nullptr));
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
@@ -1660,7 +1686,8 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
   const int ntb = H * W <= 4096 ? 256 : 512;
   const bool ok = launch_ra<false, true, false, true, false>(
       ntb, nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, B, C,
-      H, W, dy, y, s, coef, nullptr, nullptr, nullptr, nullptr, st);
+      H, W, dy, y, s, coef, nullptr, nullptr, nullptr, nullptr, st, nullptr, nullptr, nullptr,
+      nullptr, fold);
   SGCN_REQUIRE(ok);   // W <= 64, <= 32 elements per thread, padded plane <= 64 KiB (ops.ra_fits)
   SGCN_LAUNCH_CHECK();
   if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);

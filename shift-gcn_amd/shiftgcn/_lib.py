@@ -67,6 +67,10 @@ SIGNATURES = {
     "sgcn_bn_apply_fold": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I,
                                 _I, _I, _P]),
     "sgcn_tshift_fwd_fold": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "sgcn_tshift_bwd_bnin_fold": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I,
+                                       _I, _I, _I, _I, _P]),
+    "sgcn_bn_bwd_apply_fold": (_I, [_P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I,
+                                    _I, _I, _P]),
     "sgcn_bn_bwd_reduce": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I,
                                 _I, _P]),
     "sgcn_bn_bwd_finalize": (_I, [_P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P]),

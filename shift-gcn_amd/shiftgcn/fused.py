@@ -676,8 +676,9 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
                                         rst=s.rs.rst)
     else:
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False)
+    # (folded into its consumer: the shift_out backward, or the bn2/residual apply)
     coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
-        part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
+        part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2, defer=True)
     if kind != "conv" and so.stride == 1 and ops.ra_fits(To * V, V):
         # neither dS nor the identity-residual gradient is written: the shift_out backward
         # forms dS while staging, gcn_dx_finish forms dout*(out > 0)
@@ -699,7 +700,7 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
     dres = None
     if kind == "conv":
         coefR, g["residual.bn.weight"], g["residual.bn.bias"] = ops.bn_bwd_finalize(
-            rpart, B, Cout, B * To * V, s.rs.rst, unit.residual.bn)
+            rpart, B, Cout, B * To * V, s.rs.rst, unit.residual.bn, defer=True)
         dres = torch.empty_like(s.rs.Rc)
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, r=s.rs.Rc, rcoef=coefR, dr=dres,
                          dx=dS)
@@ -842,7 +843,7 @@ def _tcn_standalone_bwd(mod, ts, dy):
     S = ts.S
     B, C, To, V = S.shape
     part, _ = ops.bn_bwd_reduce(dy, None, False, S, ts.sst, False)
-    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, ts.sst, mod.bn2)
+    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, ts.sst, mod.bn2, defer=True)
     dS = ops.bn_bwd_apply(dy, None, False, S, coef, False)
     dH, g = tcn_core_backward(mod, ts, dS)
     g["bn2.weight"], g["bn2.bias"] = dg, db
@@ -857,7 +858,7 @@ def _convbn_standalone_fwd(mod, x, training):
 def _convbn_standalone_bwd(mod, s, dy):
     B, C, To, V = s.Rc.shape
     part, _ = ops.bn_bwd_reduce(dy, None, False, s.Rc, s.rst, False)
-    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, s.rst, mod.bn)
+    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, s.rst, mod.bn, defer=True)
     dRc = ops.bn_bwd_apply(dy, None, False, s.Rc, coef, False)
     dx = torch.zeros_like(s.x)
     g = convbn_dx_and_dw(mod, s, dRc, dx, accumulate=True)

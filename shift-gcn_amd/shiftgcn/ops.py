@@ -17,7 +17,66 @@ _F32 = torch.float32
 
 
 def _ptr(t):
-    return None if t is None else t.data_ptr()
+    if t is None:
+        return None
+    if isinstance(t, PendingCoef):   # read as a tensor: its finalize launches first
+        t = t.tensor()
+    return t.data_ptr()
+
+
+class BnBwdFoldStruct(ctypes.Structure):
+    """``sgcn_bn_bwd_fold`` (include/shiftgcn.h)."""
+    _fields_ = [("part", ctypes.c_void_p), ("mean", ctypes.c_void_p),
+                ("invstd", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
+                ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+                ("coef", ctypes.c_void_p), ("n_total", ctypes.c_double),
+                ("batch_stats", ctypes.c_int)]
+
+
+class PendingCoef:
+    """A per-channel BatchNorm backward finalize left for its consumer to fold (round 4,
+    ``bn_bwd_finalize(..., defer=True)``): ``take_fold()`` hands it to a folding consumer
+    (sgcn_tshift_bwd_bnin_fold, sgcn_bn_bwd_apply_fold), whose plane workgroups write the
+    coefficients and dgamma/dbeta; ``tensor()`` (or any other use) launches
+    sgcn_bn_bwd_finalize first."""
+
+    __slots__ = ("t", "_spec")
+
+    def __init__(self, coef, spec):
+        self.t, self._spec = coef, spec
+
+    @property
+    def pending(self):
+        return self._spec is not None
+
+    def tensor(self):
+        spec, self._spec = self._spec, None
+        if spec is not None:
+            part, B, F, n_total, st, bn, dgamma, dbeta = spec
+            part.record_stream(torch.cuda.current_stream(part.device))
+            with _timed("finalize", 0, 4 * part.numel(), part):
+                rc = _lib.load().sgcn_bn_bwd_finalize(
+                    _ptr(part), B, F, int(n_total), 0, _ptr(st.mean), _ptr(st.invstd),
+                    _ptr(bn.weight), _ptr(dgamma), _ptr(dbeta), 0, int(st.batch), _ptr(self.t),
+                    _stream(part))
+            _lib.check(rc, "sgcn_bn_bwd_finalize")
+        return self.t
+
+    def take_fold(self):
+        spec, self._spec = self._spec, None
+        if spec is None:
+            return None
+        part, B, F, n_total, st, bn, dgamma, dbeta = spec
+        part.record_stream(torch.cuda.current_stream(part.device))
+        f = BnBwdFoldStruct(_ptr(part), _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
+                            _ptr(dgamma), _ptr(dbeta), _ptr(self.t), float(n_total),
+                            int(st.batch))
+        return f, part
+
+
+def _fold_of(c):
+    """(struct, keep) if ``c`` is a pending backward finalize, else None."""
+    return c.take_fold() if isinstance(c, PendingCoef) and c.pending else None
 
 
 # --------------------------------------------------------------------------------------
@@ -440,8 +499,12 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False, pos_out=No
     """Stride-1 shift backward (ReLU mask on ``inp``) whose output gradient is the input
     gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3 (s = that
     BatchNorm's input), formed in the kernel. Returns (grad_input, grad_xpos, grad_ypos)."""
-    for t, n in ((dy, "dy"), (y, "y"), (s, "s"), (coef, "coef"), (inp, "input")):
+    fold = _fold_of(coef)
+    for t, n in ((dy, "dy"), (y, "y"), (s, "s"), (inp, "input")):
         check_input(t, n)
+    if fold is None:
+        coef = coef.tensor() if isinstance(coef, PendingCoef) else coef
+        check_input(coef, "coef")
     B, C, H, W = inp.shape
     lib = _lib.load()
     dev = inp.device
@@ -451,10 +514,11 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False, pos_out=No
     gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev, pos_out)
     nb = 4 * (3 * dy.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
-        rc = lib.sgcn_tshift_bwd_bnin(_ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp),
-                                      _ptr(xpos), _ptr(ypos), _ptr(gin), _ptr(gx), _ptr(gy),
-                                      _ptr(ws), nbytes, B, C, H, W, 1, _stream(inp))
-    _lib.check(rc, "sgcn_tshift_bwd_bnin")
+        rc = lib.sgcn_tshift_bwd_bnin_fold(
+            _ptr(dy), _ptr(y), _ptr(s), None if fold else _ptr(coef),
+            ctypes.byref(fold[0]) if fold else None, _ptr(inp), _ptr(xpos), _ptr(ypos),
+            _ptr(gin), _ptr(gx), _ptr(gy), _ptr(ws), nbytes, B, C, H, W, 1, _stream(inp))
+    _lib.check(rc, "sgcn_tshift_bwd_bnin_fold")
     return gin, (pp if pp is not None else gx), gy
 
 
@@ -818,12 +882,16 @@ def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats =
     return part, rpart
 
 
-def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
-    """Returns (coef[3,F], dgamma, dbeta) with dgamma/dbeta in the module's layout."""
+def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0, defer=False):
+    """Returns (coef[3,F], dgamma, dbeta) with dgamma/dbeta in the module's layout.
+    ``defer`` (per-channel only): coef is a PendingCoef that its consumer folds (dgamma /
+    dbeta are then written by that consumer's launch)."""
     dev = part.device
     coef = torch.empty((3, F), device=dev, dtype=_F32)
     dgamma = grad_like(bn.weight) if bn.weight is not None else None
     dbeta = grad_like(bn.bias) if bn.bias is not None else None
+    if defer and FOLD_FINALIZE and perm_V == 0:
+        return PendingCoef(coef, (part, B, F, n_total, st, bn, dgamma, dbeta)), dgamma, dbeta
     with _timed("finalize", 0, 4 * part.numel(), part):
         rc = _lib.load().sgcn_bn_bwd_finalize(_ptr(part), B, F, int(n_total), perm_V,
                                               _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
@@ -856,12 +924,16 @@ def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, d
     B, C, T, V = x.shape
     dx = torch.empty_like(x) if dx is None else dx
     nb = 4 * x.numel() * (3 + (y is not None) + (r is not None) + (dr is not None))
-    with _timed("bn_bwd_apply", 0, nb, x, _shp(x)):
-        rc = _lib.load().sgcn_bn_bwd_apply(_ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(coef),
-                                           int(per_joint), _ptr(r), _ptr(rcoef),
-                                           _ptr(dy_coef), _ptr(dx), _ptr(dr), B, C, T, V,
-                                           _stream(x))
-    _lib.check(rc, "sgcn_bn_bwd_apply")
+    # pending per-channel backward finalizes are folded into this launch
+    fm = _fold_of(coef) if not per_joint else None
+    fr = _fold_of(rcoef)
+    with _timed("bn_bwd_apply", 0, nb, x, ("FOLD " if fm or fr else "") + _shp(x)):
+        rc = _lib.load().sgcn_bn_bwd_apply_fold(
+            _ptr(dy), _ptr(y), int(relu), _ptr(x), None if fm else _ptr(coef), int(per_joint),
+            ctypes.byref(fm[0]) if fm else None, _ptr(r), None if fr else _ptr(rcoef),
+            ctypes.byref(fr[0]) if fr else None, _ptr(dy_coef), _ptr(dx), _ptr(dr), B, C, T,
+            V, _stream(x))
+    _lib.check(rc, "sgcn_bn_bwd_apply_fold")
     return dx
 
 

@@ -112,3 +112,63 @@ def test_training_steps_bit_identical_with_folded_finalizes(cfg, monkeypatch):
         assert torch.equal(s0[k], s1[k]), k
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("B,C,T,V", [(4, 16, 30, 25), (3, 8, 12, 70), (2, 64, 150, 25)])
+def test_backward_apply_with_folded_finalizes(B, C, T, V, monkeypatch):
+    """bn2 + residual BatchNorm backward finalizes folded into the unit tail's backward apply
+    (sgcn_bn_bwd_apply_fold): bit-identical coefficients, dgamma/dbeta, dx and dr."""
+    from shiftgcn import ops
+    g = torch.Generator().manual_seed(3 * B + C + T + V)
+    S = torch.randn(B, C, T, V, generator=g).to(DEV)
+    R = (torch.randn(B, C, T, V, generator=g) * 2).to(DEV)
+    dy = torch.randn(B, C, T, V, generator=g).to(DEV)
+    bn1, bn2 = _bn(C, 21), _bn(C, 22)
+    st = ops.bn_finalize(ops.moments(S, False), B, C, T * V, bn1)
+    rst = ops.bn_finalize(ops.moments(R, False), B, C, T * V, bn2)
+    y = ops.bn_apply(S, st, False, r=R, rst=rst, relu=True)
+    part, rpart = ops.bn_bwd_reduce(dy, y, True, S, st, False, r=R, rst=rst)
+    res = []
+    for fold in (0, 1):
+        monkeypatch.setattr(ops, "FOLD_FINALIZE", fold)
+        coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * T * V, st, bn1, defer=True)
+        rcoef, rdg, rdb = ops.bn_bwd_finalize(rpart, B, C, B * T * V, rst, bn2, defer=True)
+        assert isinstance(coef, ops.PendingCoef) == bool(fold)
+        dx, dr = torch.empty_like(S), torch.empty_like(R)
+        ops.bn_bwd_apply(dy, y, True, S, coef, False, r=R, rcoef=rcoef, dr=dr, dx=dx)
+        torch.cuda.synchronize()
+        ct = coef.t if fold else coef
+        rt = rcoef.t if fold else rcoef
+        res.append([dx, dr, ct.clone(), rt.clone(), dg.clone(), db.clone(), rdg.clone(),
+                    rdb.clone()])
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,C,T,V", [(4, 16, 30, 25), (2, 64, 300, 25), (3, 32, 75, 33)])
+def test_shift_out_backward_with_folded_finalize(B, C, T, V, monkeypatch):
+    """bn2's backward finalize folded into the shift_out backward (sgcn_tshift_bwd_bnin_fold,
+    shift_gcn.py:72-73 + 161-162): bit-identical input and position gradients, coefficients
+    and dgamma/dbeta."""
+    from shiftgcn import ops
+    g = torch.Generator().manual_seed(5 * B + C + T + V)
+    R = torch.relu(torch.randn(B, C, T, V, generator=g) + 0.2).to(DEV)
+    xpos = ((torch.rand(C, generator=g) - 0.5) * 2e-8).to(DEV)
+    ypos = ((torch.rand(C, generator=g) - 0.5) * 4).to(DEV)
+    bn = _bn(C, 31)
+    stats = torch.empty(B * C * 2, device=DEV)
+    S = ops.tshift_fwd(R, xpos, ypos, 1, stats=stats)
+    sst = ops.bn_finalize(stats, B, C, T * V, bn)
+    out = ops.bn_apply(S, sst, False, relu=True)
+    dout = torch.randn(B, C, T, V, generator=g).to(DEV)
+    part, _ = ops.bn_bwd_reduce(dout, out, True, S, sst, False)
+    res = []
+    for fold in (0, 1):
+        monkeypatch.setattr(ops, "FOLD_FINALIZE", fold)
+        coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * T * V, sst, bn, defer=True)
+        gin, gx, gy = ops.tshift_bwd_bnin(dout, out, S, coef, R, xpos, ypos)
+        torch.cuda.synchronize()
+        ct = coef.t if fold else coef
+        res.append([gin, gx, gy, ct.clone(), dg.clone(), db.clone()])
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
