@@ -184,52 +184,60 @@ __device__ __forceinline__ void bn_running_update(float* rm, float* rv, int rf, 
   rv[rf] = (1.f - momentum) * rv[rf] + momentum * (float)c.unbiased;
 }
 
-// The folded per-channel finalize (sgcn_bn_fold): returns channel c's (scale, shift) to
-// every thread of the workgroup (call from all threads: two barriers); the workgroup of
-// sample 0 also writes the statistics and the running-stat update. The batch sums follow
-// bn_finalize_kernel's order: sample b into partial sum (b mod 8), in increasing b, then the
-// eight merged 0..7 (feature_sums).
-__device__ __forceinline__ float2 bn_fold_channel(const sgcn_bn_fold& f, int c, int C, int b,
-                                                  int B) {
+// The batch partials of channel c (part[b*C + c], b < B) as the three double sums of
+// bn_finalize_kernel's feature_sums, in ITS order — sample b into partial sum (b mod 8) in
+// increasing b, the eight merged 0..7 — so the folded coefficients are bit-identical to the
+// separate finalize's. One global round trip: every thread loads one partial into LDS, then
+// eight threads add theirs in order. NSUM = 2 (backward: sum g, sum g*xhat) or 3 (forward:
+// sum mean, sum M2, sum mean^2). Result in thread 0; call from all threads (2 barriers).
+constexpr int kFoldMaxB = 512;   // batch planes staged in LDS (more: direct loads)
+template <int NSUM>
+__device__ __forceinline__ void fold_sums(const float2* __restrict__ part, int c, int C, int B,
+                                          double (&out)[3]) {
+  __shared__ float2 pv_s[kFoldMaxB];
   __shared__ double fs[8][3];
-  __shared__ float2 fr;
-  const int t = threadIdx.x;
-  const float2* __restrict__ part = (const float2*)f.part;
+  const int t = threadIdx.x, nt = blockDim.x;
+  const bool staged = B <= kFoldMaxB;
+  if (staged)
+    for (int b = t; b < B; b += nt) pv_s[b] = part[(size_t)b * C + c];
+  __syncthreads();
   if (t < 8) {
-    double ax = 0.0, ay = 0.0, axx = 0.0;
-    int bb = t;
-    for (; bb + 24 < B; bb += 32) {   // 4 samples' loads in flight
-      float2 pv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) pv[u] = part[(size_t)(bb + 8 * u) * C + c];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        ax += pv[u].x;
-        ay += pv[u].y;
-        axx += (double)pv[u].x * pv[u].x;
-      }
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    for (int b = t; b < B; b += 8) {
+      const float2 pv = staged ? pv_s[b] : part[(size_t)b * C + c];
+      a0 += pv.x;
+      a1 += pv.y;
+      if (NSUM == 3) a2 += (double)pv.x * pv.x;
     }
-    for (; bb < B; bb += 8) {
-      const float2 pv = part[(size_t)bb * C + c];
-      ax += pv.x;
-      ay += pv.y;
-      axx += (double)pv.x * pv.x;
-    }
-    fs[t][0] = ax;
-    fs[t][1] = ay;
-    fs[t][2] = axx;
+    fs[t][0] = a0;
+    fs[t][1] = a1;
+    fs[t][2] = a2;
   }
   __syncthreads();
   if (t == 0) {
-    double ax = fs[0][0], ay = fs[0][1], axx = fs[0][2];
+    out[0] = fs[0][0];
+    out[1] = fs[0][1];
+    out[2] = fs[0][2];
     for (int q = 1; q < 8; ++q) {
-      ax += fs[q][0];
-      ay += fs[q][1];
-      axx += fs[q][2];
+      out[0] += fs[q][0];
+      out[1] += fs[q][1];
+      out[2] += fs[q][2];
     }
+  }
+}
+
+// The folded per-channel finalize (sgcn_bn_fold): returns channel c's (scale, shift) to
+// every thread of the workgroup (call from all threads: three barriers); the workgroup of
+// sample 0 also writes the statistics and the running-stat update.
+__device__ __forceinline__ float2 bn_fold_channel(const sgcn_bn_fold& f, int c, int C, int b,
+                                                  int B) {
+  __shared__ float2 fr;
+  double sm[3];
+  fold_sums<3>((const float2*)f.part, c, C, B, sm);
+  if (threadIdx.x == 0) {
     const float g = f.gamma ? f.gamma[c] : 1.f;
     const float be = f.beta ? f.beta[c] : 0.f;
-    const BnCoef k = bn_train_coef(ax, ay, axx, B, f.n_part, f.eps, g, be);
+    const BnCoef k = bn_train_coef(sm[0], sm[1], sm[2], B, f.n_part, f.eps, g, be);
     fr = make_float2(k.scale, k.shift);
     if (b == 0) {
       f.mean[c] = k.mean;
@@ -257,48 +265,20 @@ __device__ __forceinline__ float3 bn_bwd_coef(double sg, double sgx, float g, fl
 }
 
 // The folded backward finalize (sgcn_bn_bwd_fold): channel c's (k1, k2, k3) to every
-// thread (two barriers, call from all threads); sample 0's workgroup writes coef and
-// dgamma/dbeta. Sums in feature_sums order (see bn_fold_channel).
+// thread (call from all threads); sample 0's workgroup writes coef and dgamma/dbeta.
 __device__ __forceinline__ float3 bn_bwd_fold_channel(const sgcn_bn_bwd_fold& f, int c, int C,
                                                       int b, int B) {
-  __shared__ double fs[8][2];
   __shared__ float3 fr;
-  const int t = threadIdx.x;
-  const float2* __restrict__ part = (const float2*)f.part;
-  if (t < 8) {
-    double ax = 0.0, ay = 0.0;
-    int bb = t;
-    for (; bb + 24 < B; bb += 32) {
-      float2 pv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) pv[u] = part[(size_t)(bb + 8 * u) * C + c];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        ax += pv[u].x;
-        ay += pv[u].y;
-      }
-    }
-    for (; bb < B; bb += 8) {
-      const float2 pv = part[(size_t)bb * C + c];
-      ax += pv.x;
-      ay += pv.y;
-    }
-    fs[t][0] = ax;
-    fs[t][1] = ay;
-  }
-  __syncthreads();
-  if (t == 0) {
-    double sg = fs[0][0], sgx = fs[0][1];
-    for (int q = 1; q < 8; ++q) {
-      sg += fs[q][0];
-      sgx += fs[q][1];
-    }
+  double sm[3];
+  fold_sums<2>((const float2*)f.part, c, C, B, sm);
+  if (threadIdx.x == 0) {
     const float g = f.gamma ? f.gamma[c] : 1.f;
-    const float3 k = bn_bwd_coef(sg, sgx, g, f.invstd[c], f.mean[c], f.n_total, f.batch_stats);
+    const float3 k = bn_bwd_coef(sm[0], sm[1], g, f.invstd[c], f.mean[c], f.n_total,
+                                 f.batch_stats);
     fr = k;
     if (b == 0) {
-      if (f.dgamma) f.dgamma[c] = (float)sgx;
-      if (f.dbeta) f.dbeta[c] = (float)sg;
+      if (f.dgamma) f.dgamma[c] = (float)sm[1];
+      if (f.dbeta) f.dbeta[c] = (float)sm[0];
       f.coef[c] = k.x;
       f.coef[C + c] = k.y;
       f.coef[2 * C + c] = k.z;

@@ -111,7 +111,9 @@ def test_training_step_has_no_shift_in_launch(monkeypatch, min_c):
     real = ops.tshift_fwd
 
     def spy(inp, xpos, ypos, stride, scale=None, **kw):
-        calls["affine" if scale is not None else "plain"] += 1
+        # the affine comes as scale/shift, or as a BnStats (possibly a folded finalize)
+        aff = scale is not None or kw.get("affine") is not None
+        calls["affine" if aff else "plain"] += 1
         return real(inp, xpos, ypos, stride, scale=scale, **kw)
 
     monkeypatch.setattr(ops, "tshift_fwd", spy)
