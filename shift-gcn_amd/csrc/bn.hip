@@ -37,6 +37,7 @@ template <bool PER_JOINT, bool ZU = false>
 __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restrict__ x,
                                                             float2* __restrict__ part, int T,
                                                             int V, int C) {
+  SGCN_CRIT_PRIO();
   __shared__ float s1[kThreads], s2[kThreads], red[2 * kThreads / 64];
   // planes in REVERSE order: the input was just written front to back by the contraction,
   // so its last planes are still in the die-level (Infinity) cache when this pass starts,
@@ -115,6 +116,7 @@ template <int NT, int LPT, bool PER_JOINT, bool ZU>
 __global__ __launch_bounds__(NT) void moments_ja_kernel(const float* __restrict__ x,
                                                         float2* __restrict__ part, int T,
                                                         int V, int C) {
+  SGCN_CRIT_PRIO();
   __shared__ float s1[NT], s2[NT], red[2 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see moments_kernel
   const int GR = NT / V, NTJ = GR * V, tid = threadIdx.x;
@@ -227,6 +229,7 @@ __global__ __launch_bounds__(64 * kFSW) void bn_finalize_kernel(
     long long* __restrict__ num_batches, float* __restrict__ mean_out,
     float* __restrict__ invstd_out, float* __restrict__ scale_out,
     float* __restrict__ shift_out) {
+  SGCN_CRIT_PRIO();
   if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += 1;
   double smean, sm2, smean2;
   int f;
@@ -251,6 +254,7 @@ __global__ void bn_eval_coef_kernel(int F, int perm_V, const float* __restrict__
                                     float* __restrict__ invstd_out,
                                     float* __restrict__ scale_out,
                                     float* __restrict__ shift_out) {
+  SGCN_CRIT_PRIO();
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
   const int rf = ref_feature(f, perm_V, F);
@@ -280,6 +284,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     const float* __restrict__ rscale, const float* __restrict__ rshift,
     float* __restrict__ y, float2* __restrict__ ystats, const float* __restrict__ gm,
     float* __restrict__ yg, int C, int T, int V) {
+  SGCN_CRIT_PRIO();
   constexpr bool OUT_STATS = OUTX == 1, OUT_G = OUTX == 2;
   __shared__ float red[2 * kThreads / 64];
   __shared__ float gm_s[OUT_G ? kThreads : 1];   // this channel's mask column, by joint
@@ -383,6 +388,7 @@ __global__ __launch_bounds__(NT) void bn_apply_ja_kernel(
     float* __restrict__ y, float2* __restrict__ ystats, const float* __restrict__ gm,
     float* __restrict__ yg, int C, int T, int V, const sgcn_bn_fold fm = sgcn_bn_fold{},
     const sgcn_bn_fold fr = sgcn_bn_fold{}) {
+  SGCN_CRIT_PRIO();
   constexpr bool OUT_STATS = OUTX == 1, OUT_G = OUTX == 2;
   __shared__ float red[2 * NT / 64];
   const int plane = blockIdx.x, c = plane % C, rc = c % V;
@@ -479,6 +485,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const float* __restrict__ r, const float* __restrict__ rmean,
     const float* __restrict__ rinvstd, const float* __restrict__ dyc, float2* __restrict__ part,
     float2* __restrict__ rpart, int C, int T, int V) {
+  SGCN_CRIT_PRIO();
   __shared__ float s0[kThreads], s1[kThreads], red[2 * kThreads / 64];
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
@@ -571,6 +578,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_ja_kernel(
     const float* __restrict__ r, const float* __restrict__ rmean,
     const float* __restrict__ rinvstd, const float* __restrict__ dyc, float2* __restrict__ part,
     float2* __restrict__ rpart, int C, int T, int V) {
+  SGCN_CRIT_PRIO();
   __shared__ float s0[NT], s1[NT], red[2 * NT / 64];
   const int plane = blockIdx.x, c = plane % C;
   const int GR = NT / V, NTJ = GR * V, tid = threadIdx.x;
@@ -647,6 +655,7 @@ __global__ __launch_bounds__(64 * kFSW) void bn_bwd_finalize_kernel(
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
     int accumulate, int batch_stats, float* __restrict__ coef) {
+  SGCN_CRIT_PRIO();
   double sg, sgx, unused;
   int f;
   if (!feature_sums(part, B, F, sg, sgx, unused, f)) return;
@@ -683,6 +692,7 @@ __global__ __launch_bounds__(64 * kGbnW) void bn_bwd_finalize_gbn_kernel(
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
     int accumulate, int batch_stats, float* __restrict__ coef) {
+  SGCN_CRIT_PRIO();
   __shared__ double red[kGbnW - 1][6][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int f = blockIdx.x * 64 + lane;
@@ -743,6 +753,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ coef, int F, const float* __restrict__ r,
     const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
     float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V) {
+  SGCN_CRIT_PRIO();
   // PJM 3: as 2, and x is the pre-shift_out contraction output, read at the same gathered
   // (pre-rotation) index the dx store uses
   constexpr bool PER_JOINT = PJM != 0, GATH = PJM >= 2, XG = PJM == 3;
@@ -823,6 +834,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_ja_kernel(
     const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
     float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V,
     const sgcn_bn_bwd_fold fm = sgcn_bn_bwd_fold{}, const sgcn_bn_bwd_fold fr = sgcn_bn_bwd_fold{}) {
+  SGCN_CRIT_PRIO();
   static_assert(PJM == 0 || PJM == 3, "per-channel, or per-joint gathered (ZU)");
   constexpr bool PER_JOINT = PJM == 3;
   const int plane = blockIdx.x, c = plane % C, rc = c % V;
@@ -906,6 +918,7 @@ __global__ __launch_bounds__(NT) void gcn_dx_finish_ja_kernel(
     float* __restrict__ dmask_part, const float* __restrict__ ps,
     const float* __restrict__ pmean, const float* __restrict__ pinvstd,
     float2* __restrict__ bn_part, int C, int T, int V, const float* __restrict__ add2m) {
+  SGCN_CRIT_PRIO();
   __shared__ float s0[NT];
   __shared__ float red[2 * NT / 64];
   const int plane = blockIdx.x, c = plane % C, rc = c % V;
@@ -993,6 +1006,7 @@ __global__ __launch_bounds__(kThreads) void gcn_gather_kernel(const float* __res
                                                               const float* __restrict__ m,
                                                               float* __restrict__ xg, int C,
                                                               int T, int V) {
+  SGCN_CRIT_PRIO();
   __shared__ float m_s[kThreads];   // this channel's mask column, by joint
   const int plane = blockIdx.x, c = plane % C;
   const int P = T * V;
@@ -1043,6 +1057,7 @@ __global__ __launch_bounds__(kThreads) void gcn_dx_finish_kernel(
     float* __restrict__ dmask_part, const float* __restrict__ ps,
     const float* __restrict__ pmean, const float* __restrict__ pinvstd,
     float2* __restrict__ bn_part, int C, int T, int V, const float* __restrict__ add2m) {
+  SGCN_CRIT_PRIO();
   // One pass: thread i owns destination joint v' = i % V of rows t = i / V (mod G), so its
   // source joint u = (v' - c) mod V is fixed: one mask value, one dmask accumulator, and
   // the x0 factor of the mask gradient, x0[t, (u + c) mod V] = x0[t, v'], is the element

@@ -14,6 +14,19 @@
 #define SGCN_DIAG_BUILD 0
 #endif
 
+// Wave priority of the critical path's kernels (s_setprio): every kernel except the
+// weight-gradient family (pw_dw*, slab_reduce) and the optimizer-only finalizes, which run
+// on the side stream, co-resident with them on the same SIMDs. The fp32 MFMA shares the VALU
+// issue, so without it a latency-bound critical-path kernel (e.g. a BatchNorm finalize)
+// co-resident with MFMA-saturated weight-gradient waves crawled (profiles/r04_prio/). 0 = off.
+#ifndef SGCN_CRIT_PRIO_LEVEL
+#define SGCN_CRIT_PRIO_LEVEL 2
+#endif
+#define SGCN_CRIT_PRIO()                                                   \
+  do {                                                                     \
+    if (SGCN_CRIT_PRIO_LEVEL) __builtin_amdgcn_s_setprio(SGCN_CRIT_PRIO_LEVEL); \
+  } while (0)
+
 #define SGCN_LAUNCH_CHECK()                                   \
   do {                                                        \
     hipError_t e__ = hipGetLastError();                       \

@@ -31,6 +31,7 @@ __device__ __forceinline__ int clip_col(int j, int V, int M) {
 __global__ __launch_bounds__(kHT) void head_moments_kernel(const float* __restrict__ x,
                                                            float2* __restrict__ part, int C,
                                                            int T, int V, int M) {
+  SGCN_CRIT_PRIO();
   __shared__ float s1[kHT], s2[kHT];
   const int nc = blockIdx.x, n = nc / C, c = nc - n * C;
   const int J = V * M, F = J * C;
@@ -79,6 +80,7 @@ __global__ __launch_bounds__(kHT) void head_apply_kernel(const float* __restrict
                                                          const float* __restrict__ shift,
                                                          float* __restrict__ y, long long total,
                                                          int C, int T, int V, int M) {
+  SGCN_CRIT_PRIO();
   const long long i = (long long)blockIdx.x * kHT + threadIdx.x;
   if (i >= total) return;
   long long r = i;
@@ -97,6 +99,7 @@ __global__ __launch_bounds__(kHT) void head_apply_kernel(const float* __restrict
 __global__ __launch_bounds__(kHT) void head_bwd_reduce_kernel(
     const float* __restrict__ g, const float* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ invstd, float2* __restrict__ part, int C, int T, int V, int M) {
+  SGCN_CRIT_PRIO();
   __shared__ float s1[kHT], s2[kHT];
   const int nc = blockIdx.x, n = nc / C, c = nc - n * C;
   const int J = V * M, F = J * C;
@@ -149,6 +152,7 @@ __global__ __launch_bounds__(kHT) void head_bwd_reduce_kernel(
 __global__ __launch_bounds__(kHT) void head_bwd_apply_kernel(
     const float* __restrict__ g, const float* __restrict__ x, const float* __restrict__ coef,
     float* __restrict__ dx, long long total, int C, int T, int V, int M) {
+  SGCN_CRIT_PRIO();
   const long long i = (long long)blockIdx.x * kHT + threadIdx.x;
   if (i >= total) return;
   long long r = i;
@@ -167,6 +171,7 @@ __global__ __launch_bounds__(kHT) void head_bwd_apply_kernel(
 __global__ __launch_bounds__(kHT) void pool_kernel(const float* __restrict__ x,
                                                    float* __restrict__ out, int C, int M,
                                                    long long P) {
+  SGCN_CRIT_PRIO();
   __shared__ float red[2 * kHT / 64];
   const int nc = blockIdx.x, n = nc / C, c = nc - n * C;
   float acc = 0.f;
@@ -194,6 +199,7 @@ __global__ __launch_bounds__(kHT) void pool_kernel(const float* __restrict__ x,
 __global__ __launch_bounds__(kHT) void pool_bwd_kernel(const float* __restrict__ dout,
                                                        float* __restrict__ dx, long long total,
                                                        int C, int M, long long P) {
+  SGCN_CRIT_PRIO();
   const long long i0 = ((long long)blockIdx.x * kHT + threadIdx.x) * 4;
   if (i0 >= total) return;
   const float rm = 1.f / (float)M, rp = 1.f / (float)P;

@@ -192,6 +192,7 @@ __global__ void tshift_params_kernel(const float* __restrict__ xpos,
                                      const float* __restrict__ shift, int K, int V,
                                      int* __restrict__ tab) {
 #pragma clang fp contract(off)
+  SGCN_CRIT_PRIO();
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
   const float x = xpos[k], y = ypos[k];
@@ -223,6 +224,7 @@ __global__ void tshift_params_kernel(const float* __restrict__ xpos,
 template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM,
           bool TSH = false, bool EPI = false>
 __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
+  SGCN_CRIT_PRIO();
   static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
   static_assert(!EPI || !ACCUM, "the eval tail epilogue stores");
   constexpr int NT = 64 * WM * WN;
@@ -1048,6 +1050,7 @@ __global__ __launch_bounds__(256) void pw_dw_smallc_kernel(DwArgs p, int pos_per
 constexpr int kSmallM = 4;
 template <bool AMC, bool ACCUM>
 __global__ __launch_bounds__(256) void pw_fwd_smallm_kernel(FwdArgs p) {
+  SGCN_CRIT_PRIO();
   __shared__ float4 Ws[256];   // [k] -> (m0..m3), zero past M
   const int tid = threadIdx.x;
   const int K = p.K, M = p.M, V = p.V, N = p.T * V;

@@ -116,6 +116,7 @@ __global__ __launch_bounds__(kThreads) void tshift_fwd_kernel(
     const float* __restrict__ ypos, const float* __restrict__ scale,
     const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
     int Ho, int stride, int add_half) {
+  SGCN_CRIT_PRIO();
   __shared__ float red[2 * kThreads / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
@@ -196,6 +197,7 @@ __global__ __launch_bounds__(kThreads) void tshift_bwd_kernel(
     const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
     float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
     int Hb, int W, int Ho, int add_half) {
+  SGCN_CRIT_PRIO();
   __shared__ float red[2 * kThreads / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
   const int c = plane % C;
@@ -371,6 +373,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_lds_kernel(
     const float* __restrict__ ypos, const float* __restrict__ scale,
     const float* __restrict__ shift, float2* __restrict__ pstats, int C, int Hb, int W,
     int Ho, int stride, int add_half) {
+  SGCN_CRIT_PRIO();
   extern __shared__ float pl[];   // Hb*W staged input (affine applied)
   __shared__ float red[2 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
@@ -459,6 +462,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     const float* __restrict__ rs = nullptr, const float* __restrict__ rt = nullptr,
     const float* __restrict__ gm = nullptr, float* __restrict__ og = nullptr,
     const sgcn_bn_fold fa = sgcn_bn_fold{}) {
+  SGCN_CRIT_PRIO();
   static_assert(MODE != 1 || (AFFINE && RES >= 1 && !STATS), "pre: affine taps of relu(...)");
   static_assert(MODE != 2 || (!AFFINE && !STATS), "tail: plain taps");
   extern __shared__ float pl[];   // padded Hb x W input plane (affine applied) + 1 spare
@@ -603,6 +607,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pre_kernel(
     const float* __restrict__ r, const float* __restrict__ rs, const float* __restrict__ rt,
     const float* __restrict__ scale, const float* __restrict__ shift, int C, int Hb, int W,
     int Ho, int stride, int add_half) {
+  SGCN_CRIT_PRIO();
   extern __shared__ float pl[];   // Hb*W staged input
   __shared__ float zs_s[1024], zt_s[1024];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
@@ -669,6 +674,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_tail_kernel(
     const float* __restrict__ r, const float* __restrict__ rs, const float* __restrict__ rt,
     const float* __restrict__ gm, float* __restrict__ og, int C, int Hb, int W, int Ho,
     int stride, int add_half) {
+  SGCN_CRIT_PRIO();
   extern __shared__ float pl[];   // Hb*W staged input
   __shared__ float gm_s[GOUT ? 1024 : 1];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see kReverse note
@@ -730,6 +736,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_s2_kernel(
     const float* __restrict__ bn_mean, const float* __restrict__ bn_invstd,
     float* __restrict__ gin, float2* __restrict__ pgrad, float2* __restrict__ bn_part, int C,
     int Hb, int W, int Ho, int add_half) {
+  SGCN_CRIT_PRIO();
   constexpr int STRIDE = 2;
   extern __shared__ float lds[];   // [Ho*W gout][Hb*W raw input]
   __shared__ float red[4 * NT / 64];
@@ -944,6 +951,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
     const float* __restrict__ gzi, float* __restrict__ gzpart, const float* __restrict__ gd = nullptr,
     const float* __restrict__ gdm = nullptr, const float* __restrict__ gdi = nullptr,
     float* __restrict__ gdpart = nullptr, const sgcn_bn_bwd_fold gf = sgcn_bn_bwd_fold{}) {
+  SGCN_CRIT_PRIO();
   static_assert(!GBN || (AFFINE && BNP && !GP), "GBN: shift_in with BNP");
   static_assert(!GBD || GBN, "GBD extends GBN");
   extern __shared__ float lds[];   // [(H + 2*kPadRows) * WP] padded gout (GBN: >= 6*NT)
