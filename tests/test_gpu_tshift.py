@@ -49,7 +49,11 @@ def test_shift_matches_golden_bit_exact(golden, case):
                                    # global-tap kernels must agree bit for bit too
                                    (1, 4, 700, 25),
                                    # W > 64: the general (non joint-aligned) LDS walk
-                                   (1, 4, 40, 70)])
+                                   (1, 4, 40, 70),
+                                   # W = 33, 224 < T <= 248: 256 threads would need > 32
+                                   # elements each; the stride-1 backward takes 512 (ADVICE
+                                   # r03: it used to drop to the global-tap kernel)
+                                   (2, 4, 240, 33)])
 def test_shift_matches_oracle_bit_exact(shape, stride):
     B, C, H, W = shape
     rng = np.random.default_rng(B * 1000 + C * 10 + H + stride)
