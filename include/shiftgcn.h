@@ -501,6 +501,17 @@ int sgcn_sgd_chunk_elems(void);
 int sgcn_sgd_step(const void* table, const int* numel, const int* chunks, int n_chunks,
                   float momentum, int nesterov, void* stream);
 
+/* Batched small launches (round 4): several independent instances of one finalize in ONE
+ * launch, from a DEVICE table of int64 entries (pointers as integers):
+ *   sgcn_tshift_pos_finalize_many: {partials, gx, gy, B, C} per entry (sgcn_tshift_pos_finalize);
+ *     max_c = the largest C;
+ *   sgcn_mask_prep_many: {mask, m, n} per entry (sgcn_mask_prep); max_n = the largest n;
+ *   sgcn_mask_grad_finalize_many: {part, mask, dmask, B, C, V} per entry
+ *     (sgcn_mask_grad_finalize, accumulate 0); max_f = the largest C*V. */
+int sgcn_tshift_pos_finalize_many(const void* table, int n, int max_c, void* stream);
+int sgcn_mask_prep_many(const void* table, int n, int max_n, void* stream);
+int sgcn_mask_grad_finalize_many(const void* table, int n, int max_f, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * CU-masked streams (hipExtStreamCreateWithCUMask), round 4: the weight-gradient side
  * stream confined to a subset of the CUs. mask: `words` uint32, bit i = CU i of the

@@ -1126,10 +1126,40 @@ __global__ void mask_prep_kernel(const float* __restrict__ mask, float* __restri
   if (i < n) m[i] = tanhf(mask[i]) + 1.f;
 }
 
+// every unit's mask prep in one launch: table[3*i] = {mask, m, n}; blockIdx.y = entry
+__global__ void mask_prep_many_kernel(const long long* __restrict__ table) {
+  const long long* e = table + 3 * blockIdx.y;
+  const int n = (int)e[2];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const float* __restrict__ mask = reinterpret_cast<const float*>(e[0]);
+    reinterpret_cast<float*>(e[1])[i] = tanhf(mask[i]) + 1.f;
+  }
+}
+
 // dmask[u][c] (+)= (sum_b part[b][c][u]) * (1 - tanh(mask)^2); parallel over b
+__device__ __forceinline__ void mask_grad_body(const float* __restrict__ part,
+                                               const float* __restrict__ mask, int B, int C,
+                                               int V, float* __restrict__ dmask,
+                                               int accumulate);
 __global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_kernel(
     const float* __restrict__ part, const float* __restrict__ mask, int B, int C, int V,
     float* __restrict__ dmask, int accumulate) {
+  mask_grad_body(part, mask, B, C, V, dmask, accumulate);
+}
+// many (the side stream's deferred ones): table[6*i] = {part, mask, dmask, B, C, V}
+__global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_many_kernel(
+    const long long* __restrict__ table) {
+  const long long* e = table + 6 * blockIdx.y;
+  const int C = (int)e[4], V = (int)e[5];
+  if ((int)blockIdx.x * kFW >= C * V) return;
+  mask_grad_body(reinterpret_cast<const float*>(e[0]), reinterpret_cast<const float*>(e[1]),
+                 (int)e[3], C, V, reinterpret_cast<float*>(e[2]), 0);
+}
+__device__ __forceinline__ void mask_grad_body(const float* __restrict__ part,
+                                               const float* __restrict__ mask, int B, int C,
+                                               int V, float* __restrict__ dmask,
+                                               int accumulate) {
   const int F = C * V;  // part feature f = c*V + u
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * kFW + (int)(threadIdx.x >> 6);
@@ -1552,6 +1582,24 @@ int sgcn_bn_bwd_apply_fold(const float* dy, const float* y, int relu, const floa
 int sgcn_mask_prep(const float* mask, float* m, int n, void* stream) {
   SGCN_REQUIRE(mask && m && n > 0);
   mask_prep_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(mask, m, n);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_mask_prep_many(const void* table, int n, int max_n, void* stream) {
+  SGCN_REQUIRE(n >= 0 && (n == 0 || (table && max_n > 0)));
+  if (n == 0) return 0;
+  mask_prep_many_kernel<<<dim3((max_n + 255) / 256, n), 256, 0, (hipStream_t)stream>>>(
+      (const long long*)table);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
+
+int sgcn_mask_grad_finalize_many(const void* table, int n, int max_f, void* stream) {
+  SGCN_REQUIRE(n >= 0 && (n == 0 || (table && max_f > 0)));
+  if (n == 0) return 0;
+  mask_grad_finalize_many_kernel<<<dim3((max_f + kFW - 1) / kFW, n), 64 * kFW, 0,
+                                   (hipStream_t)stream>>>((const long long*)table);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

@@ -1220,9 +1220,30 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
 // up to rounding), then applyShiftConstraint (.cu:370-395) with its float/double
 // promotions: sqrt(dy*dy) in float (correctly rounded), quotients in float, times the
 // double literals 0.0 / 0.01, stored as float; the dr == 0 branch stores 0.0 / 0.0001.
+__device__ __forceinline__ void pos_finalize_body(const float2* __restrict__ pgrad, int B,
+                                                  int C, float* __restrict__ gx,
+                                                  float* __restrict__ gy);
+
 __global__ __launch_bounds__(256) void tshift_pos_finalize_kernel(
     const float2* __restrict__ pgrad, int B, int C, float* __restrict__ gx,
     float* __restrict__ gy) {
+  pos_finalize_body(pgrad, B, C, gx, gy);
+}
+
+// Many position-gradient finalizes in one launch (the side stream's deferred ones, flushed
+// at the end of the backward): table[5*i] = {partials, gx, gy, B, C}; blockIdx.y = entry.
+__global__ __launch_bounds__(256) void tshift_pos_finalize_many_kernel(
+    const long long* __restrict__ table) {
+  const long long* e = table + 5 * blockIdx.y;
+  const int C = (int)e[4];
+  if ((int)blockIdx.x * 4 >= C) return;   // whole workgroup past this entry's channels
+  pos_finalize_body(reinterpret_cast<const float2*>(e[0]), (int)e[3], C,
+                    reinterpret_cast<float*>(e[1]), reinterpret_cast<float*>(e[2]));
+}
+
+__device__ __forceinline__ void pos_finalize_body(const float2* __restrict__ pgrad, int B,
+                                                  int C, float* __restrict__ gx,
+                                                  float* __restrict__ gy) {
   // one wave per channel, lanes striding the batch (one round trip of 4 loads for
   // B <= 256), fixed xor tree in double: deterministic
   const int lane = threadIdx.x & 63;
@@ -1704,6 +1725,15 @@ int sgcn_tshift_bwd_bnin_fold(const float* dy, const float* y, const float* s,
 }
 
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C) { return (size_t)B * C * sizeof(float2); }
+
+int sgcn_tshift_pos_finalize_many(const void* table, int n, int max_c, void* stream) {
+  SGCN_REQUIRE(n >= 0 && (n == 0 || (table && max_c > 0)));
+  if (n == 0) return 0;
+  tshift_pos_finalize_many_kernel<<<dim3((max_c + 3) / 4, n), 256, 0, (hipStream_t)stream>>>(
+      (const long long*)table);
+  SGCN_LAUNCH_CHECK();
+  return 0;
+}
 
 int sgcn_tshift_pos_finalize(const void* ws, int B, int C, float* gx, float* gy, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && ws && gx && gy);

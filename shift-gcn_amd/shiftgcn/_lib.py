@@ -95,6 +95,9 @@ SIGNATURES = {
     "sgcn_head_bwd_apply": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "sgcn_pool": (_I, [_P, _P, _I, _I, _I, _L, _P]),
     "sgcn_pool_bwd": (_I, [_P, _P, _I, _I, _I, _L, _P]),
+    "sgcn_tshift_pos_finalize_many": (_I, [_P, _I, _I, _P]),
+    "sgcn_mask_prep_many": (_I, [_P, _I, _I, _P]),
+    "sgcn_mask_grad_finalize_many": (_I, [_P, _I, _I, _P]),
     "sgcn_device_cu_count": (_I, [_I, _P]),
     "sgcn_stream_create_cu_mask": (_I, [_P, _I, _P]),
     "sgcn_stream_get_cu_mask": (_I, [_P, _P, _I]),

@@ -151,16 +151,48 @@ class _OffPath:
             torch.cuda.current_stream(self.tensors[0].device).wait_event(self.ev)
 
 
+# Optimizer-only finalizes of a backward on the side stream (position gradients, mask
+# gradients), deferred and launched together when the backward joins the side stream
+# (join_side): one launch per kind instead of one per unit (SGCN_BATCH_SIDE=0: each its own
+# side-stream launch, as before). Per device: {"pos": [...], "mask": [...]}.
+BATCH_SIDE = int(os.environ.get("SGCN_BATCH_SIDE", "1"))
+_DEFER = {}
+
+
+def _deferred(device):
+    d = _DEFER.get(device)
+    if d is None:
+        d = _DEFER[device] = {"pos": [], "mask": []}
+    return d
+
+
 def _pos_grads(gx, gy, shift):
     """A shift backward's (grad_xpos, grad_ypos): as returned, or, when its partials were
     left for later (ops.PosPartials), finalized on the side stream into gradient tensors
-    allocated here."""
+    allocated here (batched with the backward's others when BATCH_SIDE)."""
     if not isinstance(gx, ops.PosPartials):
         return gx, gy
     ox, oy = ops.grad_like(shift.xpos), ops.grad_like(shift.ypos)
+    if BATCH_SIDE:
+        _deferred(gx.ws.device)["pos"].append((gx, ox, oy))
+        return ox, oy
     with _OffPath(True, gx.ws):
         gx.finalize(ox, oy)
     return ox, oy
+
+
+def _flush_deferred(device):
+    """Launch the backward's deferred optimizer-only finalizes on the side stream (after
+    everything enqueued on the current stream, which made their partials)."""
+    d = _DEFER.get(device)
+    if not d or not (d["pos"] or d["mask"]):
+        return
+    pos, mask = d["pos"], d["mask"]
+    d["pos"], d["mask"] = [], []
+    keep = [e[0].ws for e in pos] + [e[0] for e in mask]
+    with _OffPath(True, *keep):
+        ops.pos_finalize_many(pos)
+        ops.mask_grad_finalize_many(mask)
 
 
 def _pos_alloc(shift, off):
@@ -170,7 +202,9 @@ def _pos_alloc(shift, off):
 
 
 def join_side(device):
-    """Make the current stream wait for every launch enqueued on the side stream."""
+    """Launch the deferred side-stream finalizes, then make the current stream wait for
+    every launch enqueued on the side stream."""
+    _flush_deferred(device)
     s = _SIDE.get(device)
     if s is not None:
         torch.cuda.current_stream(device).wait_stream(s)
@@ -203,7 +237,7 @@ def gcn_forward(mod, x0, training, off=False):
     if cache is not None and cache[0] is x0:
         xg, m = cache[1], cache[2]    # made by the previous unit's tail from its registers
     else:
-        m = ops.mask_prep(mod.Feature_Mask)
+        m = _mask_of(mod)
         xg = ops.gcn_gather(x0, m)    # shift_in gather * mask, once (reused by the dW)
     Z = _empty(B, Cout, T, V, like=x0)
     # Z is stored BEFORE shift_out (plain contraction stores) and the BatchNorm kernels
@@ -222,6 +256,22 @@ def gcn_forward(mod, x0, training, off=False):
     s.x0, s.xg, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, xg, Z, zst, D0, dst, H, m
     s.h_moments = hm   # moments of H for Shift_tcn.bn, produced by the same launch
     return H, s
+
+
+def _mask_of(gcn):
+    """tanh(Feature_Mask) + 1 of a Shift_gcn: the one linked_units prepared for this call
+    (all units' in one launch), else its own launch."""
+    r = gcn.__dict__.get("_mask_ready")
+    if r is not None and r[0] is gcn.Feature_Mask and r[1] == gcn.Feature_Mask._version:
+        return r[2]
+    return ops.mask_prep(gcn.Feature_Mask)
+
+
+def prepare_masks(gcns):
+    """Every Shift_gcn's mask for one forward in one launch (sgcn_mask_prep_many)."""
+    ms = ops.mask_prep_many([g.Feature_Mask for g in gcns])
+    for g, m in zip(gcns, ms):
+        g.__dict__["_mask_ready"] = (g.Feature_Mask, g.Feature_Mask._version, m)
 
 
 def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, extra_out=None,
@@ -285,8 +335,11 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     else:
         dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
     dmask = ops.grad_like(mod.Feature_Mask)
-    with _OffPath(off, mpart):
-        ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V, out=dmask)
+    if off and BATCH_SIDE:   # with the backward's other optimizer-only finalizes (join_side)
+        _deferred(mpart.device)["mask"].append((mpart, mod.Feature_Mask, B, Cin, V, dmask))
+    else:
+        with _OffPath(off, mpart):
+            ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V, out=dmask)
     g["Feature_Mask"] = dmask
     if mod.has_down:
         dWd = ops.grad_like(conv.weight)
@@ -344,7 +397,7 @@ def gcn_infer_h(mod, x0):
     if cache is not None and cache[0] is x0:
         xg = cache[1]
     else:
-        xg = ops.gcn_gather(x0, ops.mask_prep(mod.Feature_Mask))
+        xg = ops.gcn_gather(x0, _mask_of(mod))
     if mod.has_down:
         w, b = folded_conv_bn(mod.down[0], mod.down[1])
         res = _empty(B, Cout, T, V, like=x0)
@@ -380,7 +433,7 @@ def gcn_infer_z(mod, x0):
     if cache is not None and cache[0] is x0:
         xg = cache[1]
     else:
-        xg = ops.gcn_gather(x0, ops.mask_prep(mod.Feature_Mask))
+        xg = ops.gcn_gather(x0, _mask_of(mod))
     Z = _empty(B, Cout, T, V, like=x0)
     ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z, 1, +1), Cout, Cin, T, V)
     zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
@@ -568,7 +621,7 @@ def unit_forward(unit, x, training):
                 r, rst, _ = convbn_core_forward(unit.residual, x, training)
         elif unit.residual_kind == "identity":
             r = x
-        gm = ops.mask_prep(consumer.Feature_Mask) if consumer is not None else None
+        gm = _mask_of(consumer) if consumer is not None else None
         out, xg_next = tcn_core_forward(unit.tcn1, H, training, tail=(r, rst, gm),
                                         pre=pre)
         if gm is not None:
@@ -587,9 +640,12 @@ def unit_forward(unit, x, training):
     # a tiny kernel, made on the side stream off the critical path
     mp = None
     if consumer is not None:
-        mp = _OffPath(off, consumer.Feature_Mask)
-        with mp:
-            gm = ops.mask_prep(consumer.Feature_Mask)
+        if "_mask_ready" in consumer.__dict__:   # prepared with the chain's others
+            gm = _mask_of(consumer)
+        else:
+            mp = _OffPath(off, consumer.Feature_Mask)
+            with mp:
+                gm = ops.mask_prep(consumer.Feature_Mask)
     H, gs = gcn_forward(unit.gcn1, x, training, off=off)
     rs = None
     if unit.residual_kind == "conv":
@@ -602,7 +658,7 @@ def unit_forward(unit, x, training):
     # its gathered, masked input is written by this tail launch too
     if mp is not None:
         mp.wait()
-    else:
+    elif consumer is None:
         gm = None
     if unit.residual_kind == "conv":
         res.wait()

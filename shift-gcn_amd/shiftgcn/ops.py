@@ -946,6 +946,79 @@ def mask_prep(mask):
     return m
 
 
+def _device_table(rows, dev):
+    """int64 rows -> a device tensor (pinned staging, copied on the current stream)."""
+    t = torch.tensor(rows, dtype=torch.int64)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
+_MASK_TABLES = {}   # (mask addresses, sizes) -> (device table, output buffers)
+
+
+def mask_prep_many(masks):
+    """tanh(mask) + 1 of several Feature_Masks in ONE launch (sgcn_mask_prep_many). The
+    device table and the output buffers are made once per set of mask tensors and reused
+    (every call recomputes the outputs), so no host copy is enqueued after the first call
+    (hipGraph capture of a forward is safe once it has run eagerly). A buffer a previous
+    forward saved for its backward is rewritten with the same values unless the masks
+    changed, i.e. an optimizer step, which comes after that backward."""
+    if not masks:
+        return []
+    for mk in masks:
+        check_input(mk, "Feature_Mask")
+    key = tuple((mk.data_ptr(), mk.numel()) for mk in masks)
+    hit = _MASK_TABLES.get(key)
+    if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            return [mask_prep(mk) for mk in masks]   # no host copy inside a capture
+        outs = [torch.empty_like(mk) for mk in masks]
+        rows = []
+        for mk, o in zip(masks, outs):
+            rows += [mk.data_ptr(), o.data_ptr(), mk.numel()]
+        hit = _MASK_TABLES[key] = (_device_table(rows, masks[0].device), outs)
+    tab, outs = hit
+    with _timed("finalize", 0, 8 * sum(m.numel() for m in masks), masks[0]):
+        rc = _lib.load().sgcn_mask_prep_many(_ptr(tab), len(masks),
+                                            max(m.numel() for m in masks), _stream(tab))
+    _lib.check(rc, "sgcn_mask_prep_many")
+    return outs
+
+
+def pos_finalize_many(entries):
+    """Several deferred position-gradient finalizes [(PosPartials, gx, gy)] in ONE launch
+    (sgcn_tshift_pos_finalize_many), on the current stream."""
+    if not entries:
+        return
+    rows = []
+    for pp, gx, gy in entries:
+        check_input(gx, "gx")
+        check_input(gy, "gy")
+        rows += [pp.ws.data_ptr(), gx.data_ptr(), gy.data_ptr(), pp.B, pp.C]
+    tab = _device_table(rows, entries[0][1].device)
+    with _timed("finalize", 0, sum(pp.ws.numel() * 4 for pp, _, _ in entries), tab):
+        rc = _lib.load().sgcn_tshift_pos_finalize_many(_ptr(tab), len(entries),
+                                                      max(pp.C for pp, _, _ in entries),
+                                                      _stream(tab))
+    _lib.check(rc, "sgcn_tshift_pos_finalize_many")
+
+
+def mask_grad_finalize_many(entries):
+    """Several deferred mask-gradient finalizes [(part, mask, B, C, V, dmask)] in ONE launch
+    (sgcn_mask_grad_finalize_many), on the current stream."""
+    if not entries:
+        return
+    rows = []
+    for part, mask, B, C, V, dmask in entries:
+        check_input(dmask, "dmask")
+        rows += [part.data_ptr(), mask.data_ptr(), dmask.data_ptr(), B, C, V]
+    tab = _device_table(rows, entries[0][0].device)
+    with _timed("finalize", 0, sum(e[0].numel() * 4 for e in entries), tab):
+        rc = _lib.load().sgcn_mask_grad_finalize_many(_ptr(tab), len(entries),
+                                                     max(e[3] * e[4] for e in entries),
+                                                     _stream(tab))
+    _lib.check(rc, "sgcn_mask_grad_finalize_many")
+
+
 def gcn_gather(x0, m):
     B, C, T, V = x0.shape
     xg = torch.empty_like(x0)

@@ -223,6 +223,8 @@ def linked_units(units):
             u.__dict__["_next_unit"] = nxt
         for u in units:
             u.__dict__["_off_path"] = True
+        # every unit's tanh(Feature_Mask) + 1 in one launch (fused.prepare_masks)
+        fused.prepare_masks([u.gcn1 for u in units])
         yield
     finally:
         for u in units:
@@ -231,3 +233,4 @@ def linked_units(units):
             u.__dict__.pop("_off_path", None)
             u.__dict__.pop("_prev_tail", None)
             u.gcn1.__dict__.pop("_gather_cache", None)
+            u.gcn1.__dict__.pop("_mask_ready", None)
