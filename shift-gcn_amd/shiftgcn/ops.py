@@ -971,6 +971,8 @@ def mask_prep_many(masks):
     if hit is None:
         if torch.cuda.is_current_stream_capturing():
             return [mask_prep(mk) for mk in masks]   # no host copy inside a capture
+        if len(_MASK_TABLES) >= 64:   # models come and go: bound the cache
+            _MASK_TABLES.clear()
         outs = [torch.empty_like(mk) for mk in masks]
         rows = []
         for mk, o in zip(masks, outs):
