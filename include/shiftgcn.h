@@ -501,16 +501,23 @@ int sgcn_sgd_chunk_elems(void);
 int sgcn_sgd_step(const void* table, const int* numel, const int* chunks, int n_chunks,
                   float momentum, int nesterov, void* stream);
 
-/* Batched small launches (round 4): several independent instances of one finalize in ONE
- * launch, from a DEVICE table of int64 entries (pointers as integers):
- *   sgcn_tshift_pos_finalize_many: {partials, gx, gy, B, C} per entry (sgcn_tshift_pos_finalize);
- *     max_c = the largest C;
- *   sgcn_mask_prep_many: {mask, m, n} per entry (sgcn_mask_prep); max_n = the largest n;
- *   sgcn_mask_grad_finalize_many: {part, mask, dmask, B, C, V} per entry
- *     (sgcn_mask_grad_finalize, accumulate 0); max_f = the largest C*V. */
-int sgcn_tshift_pos_finalize_many(const void* table, int n, int max_c, void* stream);
-int sgcn_mask_prep_many(const void* table, int n, int max_n, void* stream);
-int sgcn_mask_grad_finalize_many(const void* table, int n, int max_f, void* stream);
+/* Batched small launches (round 4): up to SGCN_BATCH_MAX independent instances of one
+ * finalize in ONE launch; the entries travel as the kernel's arguments (no table copy).
+ *   sgcn_tshift_pos_finalize_many: partials[i], gx[i], gy[i], B[i], C[i] (as
+ *     sgcn_tshift_pos_finalize);
+ *   sgcn_mask_prep_many: mask[i], m[i], n[i] (as sgcn_mask_prep);
+ *   sgcn_mask_grad_finalize_many: part[i], mask[i], dmask[i], B[i], C[i], V[i] (as
+ *     sgcn_mask_grad_finalize, accumulate 0).
+ * All arrays are HOST arrays of n <= SGCN_BATCH_MAX entries. */
+#define SGCN_BATCH_MAX 32
+int sgcn_tshift_pos_finalize_many(const void* const* partials, float* const* gx,
+                                  float* const* gy, const int* B, const int* C, int n,
+                                  void* stream);
+int sgcn_mask_prep_many(const float* const* mask, float* const* m, const int* count, int n,
+                        void* stream);
+int sgcn_mask_grad_finalize_many(const float* const* part, const float* const* mask,
+                                 float* const* dmask, const int* B, const int* C,
+                                 const int* V, int n, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * CU-masked streams (hipExtStreamCreateWithCUMask), round 4: the weight-gradient side

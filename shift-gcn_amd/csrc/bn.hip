@@ -1126,15 +1126,16 @@ __global__ void mask_prep_kernel(const float* __restrict__ mask, float* __restri
   if (i < n) m[i] = tanhf(mask[i]) + 1.f;
 }
 
-// every unit's mask prep in one launch: table[3*i] = {mask, m, n}; blockIdx.y = entry
-__global__ void mask_prep_many_kernel(const long long* __restrict__ table) {
-  const long long* e = table + 3 * blockIdx.y;
-  const int n = (int)e[2];
+// every unit's mask prep in one launch (the entries are kernel arguments); blockIdx.y = entry
+struct MaskPrepBatch {
+  const float* mask[SGCN_BATCH_MAX];
+  float* m[SGCN_BATCH_MAX];
+  int n[SGCN_BATCH_MAX];
+};
+__global__ void mask_prep_many_kernel(const MaskPrepBatch t) {
+  const int e = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const float* __restrict__ mask = reinterpret_cast<const float*>(e[0]);
-    reinterpret_cast<float*>(e[1])[i] = tanhf(mask[i]) + 1.f;
-  }
+  if (i < t.n[e]) t.m[e][i] = tanhf(t.mask[e][i]) + 1.f;
 }
 
 // dmask[u][c] (+)= (sum_b part[b][c][u]) * (1 - tanh(mask)^2); parallel over b
@@ -1147,14 +1148,19 @@ __global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_kernel(
     float* __restrict__ dmask, int accumulate) {
   mask_grad_body(part, mask, B, C, V, dmask, accumulate);
 }
-// many (the side stream's deferred ones): table[6*i] = {part, mask, dmask, B, C, V}
-__global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_many_kernel(
-    const long long* __restrict__ table) {
-  const long long* e = table + 6 * blockIdx.y;
-  const int C = (int)e[4], V = (int)e[5];
-  if ((int)blockIdx.x * kFW >= C * V) return;
-  mask_grad_body(reinterpret_cast<const float*>(e[0]), reinterpret_cast<const float*>(e[1]),
-                 (int)e[3], C, V, reinterpret_cast<float*>(e[2]), 0);
+// many (the side stream's deferred ones; the entries are kernel arguments)
+struct MaskGradBatch {
+  const float* part[SGCN_BATCH_MAX];
+  const float* mask[SGCN_BATCH_MAX];
+  float* dmask[SGCN_BATCH_MAX];
+  int B[SGCN_BATCH_MAX];
+  int C[SGCN_BATCH_MAX];
+  int V[SGCN_BATCH_MAX];
+};
+__global__ __launch_bounds__(64 * kFW) void mask_grad_finalize_many_kernel(const MaskGradBatch t) {
+  const int i = blockIdx.y;
+  if ((int)blockIdx.x * kFW >= t.C[i] * t.V[i]) return;
+  mask_grad_body(t.part[i], t.mask[i], t.B[i], t.C[i], t.V[i], t.dmask[i], 0);
 }
 __device__ __forceinline__ void mask_grad_body(const float* __restrict__ part,
                                                const float* __restrict__ mask, int B, int C,
@@ -1586,20 +1592,45 @@ int sgcn_mask_prep(const float* mask, float* m, int n, void* stream) {
   return 0;
 }
 
-int sgcn_mask_prep_many(const void* table, int n, int max_n, void* stream) {
-  SGCN_REQUIRE(n >= 0 && (n == 0 || (table && max_n > 0)));
+int sgcn_mask_prep_many(const float* const* mask, float* const* m, const int* count, int n,
+                        void* stream) {
+  SGCN_REQUIRE(n >= 0 && n <= SGCN_BATCH_MAX);
   if (n == 0) return 0;
-  mask_prep_many_kernel<<<dim3((max_n + 255) / 256, n), 256, 0, (hipStream_t)stream>>>(
-      (const long long*)table);
+  SGCN_REQUIRE(mask && m && count);
+  MaskPrepBatch t{};
+  int mx = 0;
+  for (int i = 0; i < n; ++i) {
+    SGCN_REQUIRE(mask[i] && m[i] && count[i] > 0);
+    t.mask[i] = mask[i];
+    t.m[i] = m[i];
+    t.n[i] = count[i];
+    mx = max(mx, count[i]);
+  }
+  mask_prep_many_kernel<<<dim3((mx + 255) / 256, n), 256, 0, (hipStream_t)stream>>>(t);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
 
-int sgcn_mask_grad_finalize_many(const void* table, int n, int max_f, void* stream) {
-  SGCN_REQUIRE(n >= 0 && (n == 0 || (table && max_f > 0)));
+int sgcn_mask_grad_finalize_many(const float* const* part, const float* const* mask,
+                                 float* const* dmask, const int* B, const int* C,
+                                 const int* V, int n, void* stream) {
+  SGCN_REQUIRE(n >= 0 && n <= SGCN_BATCH_MAX);
   if (n == 0) return 0;
-  mask_grad_finalize_many_kernel<<<dim3((max_f + kFW - 1) / kFW, n), 64 * kFW, 0,
-                                   (hipStream_t)stream>>>((const long long*)table);
+  SGCN_REQUIRE(part && mask && dmask && B && C && V);
+  MaskGradBatch t{};
+  int mf = 0;
+  for (int i = 0; i < n; ++i) {
+    SGCN_REQUIRE(part[i] && mask[i] && dmask[i] && B[i] > 0 && C[i] > 0 && V[i] > 0);
+    t.part[i] = part[i];
+    t.mask[i] = mask[i];
+    t.dmask[i] = dmask[i];
+    t.B[i] = B[i];
+    t.C[i] = C[i];
+    t.V[i] = V[i];
+    mf = max(mf, C[i] * V[i]);
+  }
+  mask_grad_finalize_many_kernel<<<dim3((mf + kFW - 1) / kFW, n), 64 * kFW, 0,
+                                   (hipStream_t)stream>>>(t);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

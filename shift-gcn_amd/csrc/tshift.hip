@@ -1231,14 +1231,18 @@ __global__ __launch_bounds__(256) void tshift_pos_finalize_kernel(
 }
 
 // Many position-gradient finalizes in one launch (the side stream's deferred ones, flushed
-// at the end of the backward): table[5*i] = {partials, gx, gy, B, C}; blockIdx.y = entry.
-__global__ __launch_bounds__(256) void tshift_pos_finalize_many_kernel(
-    const long long* __restrict__ table) {
-  const long long* e = table + 5 * blockIdx.y;
-  const int C = (int)e[4];
-  if ((int)blockIdx.x * 4 >= C) return;   // whole workgroup past this entry's channels
-  pos_finalize_body(reinterpret_cast<const float2*>(e[0]), (int)e[3], C,
-                    reinterpret_cast<float*>(e[1]), reinterpret_cast<float*>(e[2]));
+// at the end of the backward); the entries are kernel arguments; blockIdx.y = entry.
+struct PosBatch {
+  const float2* p[SGCN_BATCH_MAX];
+  float* gx[SGCN_BATCH_MAX];
+  float* gy[SGCN_BATCH_MAX];
+  int B[SGCN_BATCH_MAX];
+  int C[SGCN_BATCH_MAX];
+};
+__global__ __launch_bounds__(256) void tshift_pos_finalize_many_kernel(const PosBatch t) {
+  const int i = blockIdx.y;
+  if ((int)blockIdx.x * 4 >= t.C[i]) return;   // whole workgroup past this entry's channels
+  pos_finalize_body(t.p[i], t.B[i], t.C[i], t.gx[i], t.gy[i]);
 }
 
 __device__ __forceinline__ void pos_finalize_body(const float2* __restrict__ pgrad, int B,
@@ -1726,11 +1730,24 @@ int sgcn_tshift_bwd_bnin_fold(const float* dy, const float* y, const float* s,
 
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C) { return (size_t)B * C * sizeof(float2); }
 
-int sgcn_tshift_pos_finalize_many(const void* table, int n, int max_c, void* stream) {
-  SGCN_REQUIRE(n >= 0 && (n == 0 || (table && max_c > 0)));
+int sgcn_tshift_pos_finalize_many(const void* const* partials, float* const* gx,
+                                  float* const* gy, const int* B, const int* C, int n,
+                                  void* stream) {
+  SGCN_REQUIRE(n >= 0 && n <= SGCN_BATCH_MAX);
   if (n == 0) return 0;
-  tshift_pos_finalize_many_kernel<<<dim3((max_c + 3) / 4, n), 256, 0, (hipStream_t)stream>>>(
-      (const long long*)table);
+  SGCN_REQUIRE(partials && gx && gy && B && C);
+  PosBatch t{};
+  int max_c = 0;
+  for (int i = 0; i < n; ++i) {
+    SGCN_REQUIRE(partials[i] && gx[i] && gy[i] && B[i] > 0 && C[i] > 0);
+    t.p[i] = (const float2*)partials[i];
+    t.gx[i] = gx[i];
+    t.gy[i] = gy[i];
+    t.B[i] = B[i];
+    t.C[i] = C[i];
+    max_c = max(max_c, C[i]);
+  }
+  tshift_pos_finalize_many_kernel<<<dim3((max_c + 3) / 4, n), 256, 0, (hipStream_t)stream>>>(t);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
 ABI_VERSION = 21
+BATCH_MAX = 32            # include/shiftgcn.h SGCN_BATCH_MAX
 ABI_DIAG_FLAG = 0x10000   # include/shiftgcn.h SGCN_ABI_DIAG_FLAG: a diagnostic build
 EINVAL = -22
 
@@ -95,9 +96,9 @@ SIGNATURES = {
     "sgcn_head_bwd_apply": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "sgcn_pool": (_I, [_P, _P, _I, _I, _I, _L, _P]),
     "sgcn_pool_bwd": (_I, [_P, _P, _I, _I, _I, _L, _P]),
-    "sgcn_tshift_pos_finalize_many": (_I, [_P, _I, _I, _P]),
-    "sgcn_mask_prep_many": (_I, [_P, _I, _I, _P]),
-    "sgcn_mask_grad_finalize_many": (_I, [_P, _I, _I, _P]),
+    "sgcn_tshift_pos_finalize_many": (_I, [_P, _P, _P, _P, _P, _I, _P]),
+    "sgcn_mask_prep_many": (_I, [_P, _P, _P, _I, _P]),
+    "sgcn_mask_grad_finalize_many": (_I, [_P, _P, _P, _P, _P, _P, _I, _P]),
     "sgcn_device_cu_count": (_I, [_I, _P]),
     "sgcn_stream_create_cu_mask": (_I, [_P, _I, _P]),
     "sgcn_stream_get_cu_mask": (_I, [_P, _P, _I]),

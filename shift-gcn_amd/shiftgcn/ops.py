@@ -946,79 +946,64 @@ def mask_prep(mask):
     return m
 
 
-def _device_table(rows, dev):
-    """int64 rows -> a device tensor (pinned staging, copied on the current stream)."""
-    t = torch.tensor(rows, dtype=torch.int64)
-    return t.pin_memory().to(dev, non_blocking=True)
+def _arr(ctype, vals):
+    return (ctype * len(vals))(*vals)
 
 
-_MASK_TABLES = {}   # (mask addresses, sizes) -> (device table, output buffers)
+def _chunks(xs):
+    for i in range(0, len(xs), _lib.BATCH_MAX):
+        yield xs[i:i + _lib.BATCH_MAX]
 
 
 def mask_prep_many(masks):
-    """tanh(mask) + 1 of several Feature_Masks in ONE launch (sgcn_mask_prep_many). The
-    device table and the output buffers are made once per set of mask tensors and reused
-    (every call recomputes the outputs), so no host copy is enqueued after the first call
-    (hipGraph capture of a forward is safe once it has run eagerly). A buffer a previous
-    forward saved for its backward is rewritten with the same values unless the masks
-    changed, i.e. an optimizer step, which comes after that backward."""
-    if not masks:
-        return []
-    for mk in masks:
-        check_input(mk, "Feature_Mask")
-    key = tuple((mk.data_ptr(), mk.numel()) for mk in masks)
-    hit = _MASK_TABLES.get(key)
-    if hit is None:
-        if torch.cuda.is_current_stream_capturing():
-            return [mask_prep(mk) for mk in masks]   # no host copy inside a capture
-        if len(_MASK_TABLES) >= 64:   # models come and go: bound the cache
-            _MASK_TABLES.clear()
-        outs = [torch.empty_like(mk) for mk in masks]
-        rows = []
-        for mk, o in zip(masks, outs):
-            rows += [mk.data_ptr(), o.data_ptr(), mk.numel()]
-        hit = _MASK_TABLES[key] = (_device_table(rows, masks[0].device), outs)
-    tab, outs = hit
-    with _timed("finalize", 0, 8 * sum(m.numel() for m in masks), masks[0]):
-        rc = _lib.load().sgcn_mask_prep_many(_ptr(tab), len(masks),
-                                            max(m.numel() for m in masks), _stream(tab))
-    _lib.check(rc, "sgcn_mask_prep_many")
+    """tanh(mask) + 1 of several Feature_Masks in ONE launch per SGCN_BATCH_MAX
+    (sgcn_mask_prep_many; the entries are kernel arguments, nothing is copied)."""
+    outs = []
+    for ch in _chunks(list(masks)):
+        for mk in ch:
+            check_input(mk, "Feature_Mask")
+        o = [torch.empty_like(mk) for mk in ch]
+        with _timed("finalize", 0, 8 * sum(m.numel() for m in ch), ch[0]):
+            rc = _lib.load().sgcn_mask_prep_many(
+                _arr(ctypes.c_void_p, [m.data_ptr() for m in ch]),
+                _arr(ctypes.c_void_p, [t.data_ptr() for t in o]),
+                _arr(ctypes.c_int, [m.numel() for m in ch]), len(ch), _stream(ch[0]))
+        _lib.check(rc, "sgcn_mask_prep_many")
+        outs += o
     return outs
 
 
 def pos_finalize_many(entries):
-    """Several deferred position-gradient finalizes [(PosPartials, gx, gy)] in ONE launch
-    (sgcn_tshift_pos_finalize_many), on the current stream."""
-    if not entries:
-        return
-    rows = []
-    for pp, gx, gy in entries:
-        check_input(gx, "gx")
-        check_input(gy, "gy")
-        rows += [pp.ws.data_ptr(), gx.data_ptr(), gy.data_ptr(), pp.B, pp.C]
-    tab = _device_table(rows, entries[0][1].device)
-    with _timed("finalize", 0, sum(pp.ws.numel() * 4 for pp, _, _ in entries), tab):
-        rc = _lib.load().sgcn_tshift_pos_finalize_many(_ptr(tab), len(entries),
-                                                      max(pp.C for pp, _, _ in entries),
-                                                      _stream(tab))
-    _lib.check(rc, "sgcn_tshift_pos_finalize_many")
+    """Several deferred position-gradient finalizes [(PosPartials, gx, gy)] in one launch
+    per SGCN_BATCH_MAX (sgcn_tshift_pos_finalize_many), on the current stream."""
+    for ch in _chunks(list(entries)):
+        for _, gx, gy in ch:
+            check_input(gx, "gx")
+            check_input(gy, "gy")
+        with _timed("finalize", 0, sum(pp.ws.numel() * 4 for pp, _, _ in ch), ch[0][1]):
+            rc = _lib.load().sgcn_tshift_pos_finalize_many(
+                _arr(ctypes.c_void_p, [pp.ws.data_ptr() for pp, _, _ in ch]),
+                _arr(ctypes.c_void_p, [gx.data_ptr() for _, gx, _ in ch]),
+                _arr(ctypes.c_void_p, [gy.data_ptr() for _, _, gy in ch]),
+                _arr(ctypes.c_int, [pp.B for pp, _, _ in ch]),
+                _arr(ctypes.c_int, [pp.C for pp, _, _ in ch]), len(ch), _stream(ch[0][1]))
+        _lib.check(rc, "sgcn_tshift_pos_finalize_many")
 
 
 def mask_grad_finalize_many(entries):
-    """Several deferred mask-gradient finalizes [(part, mask, B, C, V, dmask)] in ONE launch
-    (sgcn_mask_grad_finalize_many), on the current stream."""
-    if not entries:
-        return
-    rows = []
-    for part, mask, B, C, V, dmask in entries:
-        check_input(dmask, "dmask")
-        rows += [part.data_ptr(), mask.data_ptr(), dmask.data_ptr(), B, C, V]
-    tab = _device_table(rows, entries[0][0].device)
-    with _timed("finalize", 0, sum(e[0].numel() * 4 for e in entries), tab):
-        rc = _lib.load().sgcn_mask_grad_finalize_many(_ptr(tab), len(entries),
-                                                     max(e[3] * e[4] for e in entries),
-                                                     _stream(tab))
-    _lib.check(rc, "sgcn_mask_grad_finalize_many")
+    """Several deferred mask-gradient finalizes [(part, mask, B, C, V, dmask)] in one launch
+    per SGCN_BATCH_MAX (sgcn_mask_grad_finalize_many), on the current stream."""
+    for ch in _chunks(list(entries)):
+        for e in ch:
+            check_input(e[5], "dmask")
+        with _timed("finalize", 0, sum(e[0].numel() * 4 for e in ch), ch[0][0]):
+            rc = _lib.load().sgcn_mask_grad_finalize_many(
+                _arr(ctypes.c_void_p, [e[0].data_ptr() for e in ch]),
+                _arr(ctypes.c_void_p, [e[1].data_ptr() for e in ch]),
+                _arr(ctypes.c_void_p, [e[5].data_ptr() for e in ch]),
+                _arr(ctypes.c_int, [e[2] for e in ch]), _arr(ctypes.c_int, [e[3] for e in ch]),
+                _arr(ctypes.c_int, [e[4] for e in ch]), len(ch), _stream(ch[0][0]))
+        _lib.check(rc, "sgcn_mask_grad_finalize_many")
 
 
 def gcn_gather(x0, m):
