@@ -174,7 +174,9 @@ def _pos_grads(gx, gy, shift):
         return gx, gy
     ox, oy = ops.grad_like(shift.xpos), ops.grad_like(shift.ypos)
     if BATCH_SIDE:
-        _deferred(gx.ws.device)["pos"].append((gx, ox, oy))
+        # written later through ALIASES: a reference to the returned tensor itself would
+        # raise its use count, and AccumulateGrad would then copy it before it is written
+        _deferred(gx.ws.device)["pos"].append((gx, ox.detach(), oy.detach()))
         return ox, oy
     with _OffPath(True, gx.ws):
         gx.finalize(ox, oy)
@@ -336,7 +338,8 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
         dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
     dmask = ops.grad_like(mod.Feature_Mask)
     if off and BATCH_SIDE:   # with the backward's other optimizer-only finalizes (join_side)
-        _deferred(mpart.device)["mask"].append((mpart, mod.Feature_Mask, B, Cin, V, dmask))
+        _deferred(mpart.device)["mask"].append((mpart, mod.Feature_Mask, B, Cin, V,
+                                                dmask.detach()))   # (alias: see _pos_grads)
     else:
         with _OffPath(off, mpart):
             ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V, out=dmask)
