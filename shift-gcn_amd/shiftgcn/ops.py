@@ -790,9 +790,12 @@ class BnStats:
         return f, part
 
 
-# Per-channel training finalizes left pending for their consumer to fold (round 4;
-# SGCN_FOLD_FINALIZE=0: every finalize its own launch, A/B knob)
-FOLD_FINALIZE = int(__import__("os").environ.get("SGCN_FOLD_FINALIZE", "1"))
+# Per-channel training finalizes left pending for their consumer to fold (round 4, A/B knob
+# SGCN_FOLD_FINALIZE=1). Off by default: measured -1.4 % on the NTU step (the consumer's
+# 8,192 plane workgroups each gathering their channel's B partials, one cache line per
+# sample at the [sample][channel] stride, cost more than the 25 launches they remove;
+# profiles/r04_fold/).
+FOLD_FINALIZE = int(__import__("os").environ.get("SGCN_FOLD_FINALIZE", "0"))
 
 
 def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True, defer=False):
