@@ -183,16 +183,17 @@ def _pos_grads(gx, gy, shift):
     return ox, oy
 
 
-def _flush_deferred(device):
-    """Launch the backward's deferred optimizer-only finalizes on the side stream (after
-    everything enqueued on the current stream, which made their partials)."""
+def _flush_deferred(device, side=True):
+    """Launch the backward's deferred optimizer-only finalizes, on the side stream (after
+    everything enqueued on the current stream, which made their partials) or, for a
+    backward that did not use it, on the current stream."""
     d = _DEFER.get(device)
     if not d or not (d["pos"] or d["mask"]):
         return
     pos, mask = d["pos"], d["mask"]
     d["pos"], d["mask"] = [], []
     keep = [e[0].ws for e in pos] + [e[0] for e in mask]
-    with _OffPath(True, *keep):
+    with _OffPath(side, *keep):
         ops.pos_finalize_many(pos)
         ops.mask_grad_finalize_many(mask)
 
@@ -337,7 +338,10 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     else:
         dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
     dmask = ops.grad_like(mod.Feature_Mask)
-    if off and BATCH_SIDE:   # with the backward's other optimizer-only finalizes (join_side)
+    # (deferred only when autograd will TAKE dmask as .grad: an existing .grad would be
+    # accumulated into from dmask before the deferred launch writes it)
+    if BATCH_SIDE and mod.Feature_Mask.grad is None and (off or _flush_queued(mpart.device)):
+        # with the backward's other optimizer-only finalizes (join_side / end of backward)
         _deferred(mpart.device)["mask"].append((mpart, mod.Feature_Mask, B, Cin, V,
                                                 dmask.detach()))   # (alias: see _pos_grads)
     else:
@@ -693,6 +697,20 @@ def _gcn_z(unit, s: UnitSaved):
     if unit.gcn1.has_down:
         return (s.gs.Z, s.gs.zst, (s.gs.D0, s.gs.dst)) if GBN_FUSION >= 2 else None
     return (s.gs.Z, s.gs.zst)
+
+
+def _flush_queued(device):
+    """In a backward without the side stream, queue (once per backward) the flush of the
+    deferred mask-gradient finalizes on the current stream at its end; False outside a
+    backward (nothing is deferred then)."""
+    if torch.is_grad_enabled():
+        return False   # create_graph backward: run in order
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(
+            lambda dev=device: _flush_deferred(dev, side=False))
+    except RuntimeError:
+        return False
+    return True
 
 
 def _off_path_ok(unit, s: UnitSaved):
