@@ -340,7 +340,10 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     dmask = ops.grad_like(mod.Feature_Mask)
     # (deferred only when autograd will TAKE dmask as .grad: an existing .grad would be
     # accumulated into from dmask before the deferred launch writes it)
-    if BATCH_SIDE and mod.Feature_Mask.grad is None and (off or _flush_queued(mpart.device)):
+    fm = mod.Feature_Mask
+    if (BATCH_SIDE and fm.grad is None and not getattr(fm, "_backward_hooks", None) and
+            not getattr(fm, "_post_accumulate_grad_hooks", None) and
+            (off or _flush_queued(mpart.device))):
         # with the backward's other optimizer-only finalizes (join_side / end of backward)
         _deferred(mpart.device)["mask"].append((mpart, mod.Feature_Mask, B, Cin, V,
                                                 dmask.detach()))   # (alias: see _pos_grads)
