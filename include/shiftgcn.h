@@ -80,20 +80,6 @@ typedef struct sgcn_bn_bwd_fold {
   int batch_stats;
 } sgcn_bn_bwd_fold;
 
-/* A training-mode BatchNorm finalize run in the TAIL of the launch that produces its
- * partials (round 4): each (sample, channel) plane workgroup stores its partials at device
- * coherence and counts itself in count[channel]; the workgroup that completes a channel
- * merges the channel's B partials in sgcn_bn_finalize's order (bit-identical values) and
- * writes its features' mean/invstd/scale/shift and running statistics (f as sgcn_bn_fold;
- * f.part is ignored: the producer's own partials; per-joint features are f = c*V + v with
- * reference order v*C + c). No finalize launch. count: >= C counters, zero on entry and
- * returned to zero by the launch — one array per stream (launches sharing one must not
- * overlap). Producers: sgcn_moments_fin. */
-typedef struct sgcn_bn_fin {
-  sgcn_bn_fold f;
-  unsigned int* count;
-} sgcn_bn_fin;
-
 /* ------------------------------------------------------------------------------------
  * Temporal shift
  * ------------------------------------------------------------------------------------ */
@@ -322,11 +308,6 @@ size_t sgcn_moments_ws_bytes(int B, int C, int V, int per_joint);
 /* part[b][f] = {mean, M2} of x over the plane (or over t per joint). */
 int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int per_joint,
                  void* stream);
-/* sgcn_moments with the BatchNorm finalize in its tail (fin NULL = sgcn_moments): the
- * statistics of BatchNorm2d (per_joint 0, n_part = T*V) or of the per-joint BatchNorm1d
- * (per_joint 3, n_part = T, F = C*V). */
-int sgcn_moments_fin(const float* x, float* part, int B, int C, int T, int V, int per_joint,
-                     const sgcn_bn_fin* fin, void* stream);
 
 /* Merge B partials (n_part elements each) per feature: batch mean / biased var ->
  * mean, invstd, scale = gamma*invstd, shift = beta - mean*scale (all [F], local feature

@@ -33,11 +33,10 @@ constexpr int kUM = 8;   // loads in flight per thread (a single-input reduction
 // ZU (per_joint = 3): x holds the Shift_gcn contraction output BEFORE its shift_out, so
 // its joint v is the logical joint (v + c) mod V (shift_gcn.py:114-118,136: z[w] =
 // y[(w - c) mod V]); the partial goes to the logical feature.
-// FIN: the BatchNorm finalize in this launch's tail (sgcn_bn_fin, channel_done).
-template <bool PER_JOINT, bool ZU = false, bool FIN = false>
+template <bool PER_JOINT, bool ZU = false>
 __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restrict__ x,
                                                             float2* __restrict__ part, int T,
-                                                            int V, int C, const BnFin fn) {
+                                                            int V, int C) {
   SGCN_CRIT_PRIO();
   __shared__ float s1[kThreads], s2[kThreads], red[2 * kThreads / 64];
   // planes in REVERSE order: the input was just written front to back by the contraction,
@@ -78,9 +77,7 @@ __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restri
         w = i + (plane % C) % V;
         w = w >= V ? w - V : w;
       }
-      const float2 pv = make_float2(xp[i] + ta / n, tq - ta * ta / n);
-      if (FIN) store_part(part + (size_t)plane * V + w, pv);
-      else part[(size_t)plane * V + w] = pv;
+      part[(size_t)plane * V + w] = make_float2(xp[i] + ta / n, tq - ta * ta / n);
     }
   } else {
     const float k0 = xp[0];
@@ -99,27 +96,26 @@ __global__ __launch_bounds__(kThreads) void moments_kernel(const float* __restri
     block_sum2(a, q, red);
     if (i == 0) {
       const float n = (float)P;
-      const float2 pv = make_float2(k0 + a / n, q - a * a / n);
-      if (FIN) store_part(part + plane, pv);
-      else part[plane] = pv;
+      part[plane] = make_float2(k0 + a / n, q - a * a / n);
     }
-  }
-  if (FIN) {
-    if (threadIdx.x >= kWave) return;   // (the partials were stored by wave 0)
-    if (channel_done(fn.count, plane % C, gridDim.x / C))
-      bn_fin_channel(fn, plane % C, C, gridDim.x / C);
   }
 }
 
+__device__ __forceinline__ int ref_feature(int f, int perm_V, int F) {
+  if (perm_V <= 0) return f;
+  const int D = F / perm_V;
+  const int d = f / perm_V, v = f - d * perm_V;
+  return v * D + d;  // BatchNorm1d(V*C) feature index of (d, v)  (shift_gcn.py:135-137)
+}
 
 // Plane-resident form of moments_kernel (V <= 64, <= 32 elements per thread): the plane's
 // loads all in flight, dealt on the joint-aligned stride NTJ = (NT / V) * V (a thread's
 // joint is fixed: the per-joint sums stay in registers and are merged over the GR row
 // groups in fixed order). Same shifted sums (shift = the plane's / joint's first element).
-template <int NT, int LPT, bool PER_JOINT, bool ZU, bool FIN = false>
+template <int NT, int LPT, bool PER_JOINT, bool ZU>
 __global__ __launch_bounds__(NT) void moments_ja_kernel(const float* __restrict__ x,
                                                         float2* __restrict__ part, int T,
-                                                        int V, int C, const BnFin fn) {
+                                                        int V, int C) {
   SGCN_CRIT_PRIO();
   __shared__ float s1[NT], s2[NT], red[2 * NT / 64];
   const int plane = gridDim.x - 1 - blockIdx.x;   // reverse: see moments_kernel
@@ -157,23 +153,14 @@ __global__ __launch_bounds__(NT) void moments_ja_kernel(const float* __restrict_
         wo = tid + (plane % C) % V;
         wo = wo >= V ? wo - V : wo;
       }
-      const float2 pv = make_float2(xp[tid] + ta / n, tq - ta * ta / n);
-      if (FIN) store_part(part + (size_t)plane * V + wo, pv);
-      else part[(size_t)plane * V + wo] = pv;
+      part[(size_t)plane * V + wo] = make_float2(xp[tid] + ta / n, tq - ta * ta / n);
     }
   } else {
     block_sum2(a, q, red);
     if (tid == 0) {
       const float n = (float)P;
-      const float2 pv = make_float2(k0 + a / n, q - a * a / n);
-      if (FIN) store_part(part + plane, pv);
-      else part[plane] = pv;
+      part[plane] = make_float2(k0 + a / n, q - a * a / n);
     }
-  }
-  if (FIN) {
-    if (threadIdx.x >= kWave) return;   // (the partials were stored by wave 0)
-    if (channel_done(fn.count, plane % C, gridDim.x / C))
-      bn_fin_channel(fn, plane % C, C, gridDim.x / C);
   }
 }
 
@@ -1221,16 +1208,28 @@ int ja_lpt(int T, int V, int nt) {
   return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 24 ? 24 : (per <= 32 ? 32 : 0)));
 }
 
-namespace {
-template <bool FIN>
-int launch_moments(const float* x, float* part, int B, int C, int T, int V, int per_joint,
-                   const BnFin& fn, hipStream_t st) {
+#define SGCN_PLANE_CHECK() \
+  SGCN_REQUIRE(B >= 0 && C > 0 && T >= 0 && V > 0 && V <= kThreads)
+
+extern "C" {
+
+size_t sgcn_moments_ws_bytes(int B, int C, int V, int per_joint) {
+  return (size_t)B * C * (per_joint ? V : 1) * sizeof(float2);
+}
+
+int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int per_joint,
+                 void* stream) {
+  SGCN_PLANE_CHECK();
+  if (B == 0) return 0;
+  SGCN_REQUIRE(x && part && T > 0);
+  hipStream_t st = (hipStream_t)stream;
+  SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
   {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
     const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
 #define SGCN_MJ(NT, L, PJ)                                                                     \
-  moments_ja_kernel<NT, L, PJ, PJ, FIN><<<B * C, NT, 0, st>>>(x, (float2*)part, T, V, C, fn)
+  moments_ja_kernel<NT, L, PJ, PJ><<<B * C, NT, 0, st>>>(x, (float2*)part, T, V, C)
 #define SGCN_MJ_L(NT, PJ)                                                                      \
   do {                                                                                         \
     if (lpt == 8) SGCN_MJ(NT, 8, PJ); else if (lpt == 16) SGCN_MJ(NT, 16, PJ);                 \
@@ -1246,53 +1245,10 @@ int launch_moments(const float* x, float* part, int B, int C, int T, int V, int 
     }
   }
   if (per_joint == 3)
-    moments_kernel<true, true, FIN><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C, fn);
-  else moments_kernel<false, false, FIN><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C, fn);
+    moments_kernel<true, true><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
+  else moments_kernel<false><<<B * C, kThreads, 0, st>>>(x, (float2*)part, T, V, C);
   SGCN_LAUNCH_CHECK();
   return 0;
-}
-}  // namespace
-
-#define SGCN_PLANE_CHECK() \
-  SGCN_REQUIRE(B >= 0 && C > 0 && T >= 0 && V > 0 && V <= kThreads)
-
-extern "C" {
-
-size_t sgcn_moments_ws_bytes(int B, int C, int V, int per_joint) {
-  return (size_t)B * C * (per_joint ? V : 1) * sizeof(float2);
-}
-
-int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int per_joint,
-                 void* stream) {
-  return sgcn_moments_fin(x, part, B, C, T, V, per_joint, nullptr, stream);
-}
-
-int sgcn_moments_fin(const float* x, float* part, int B, int C, int T, int V, int per_joint,
-                     const sgcn_bn_fin* fin, void* stream) {
-  SGCN_PLANE_CHECK();
-  if (B == 0) return 0;
-  SGCN_REQUIRE(x && part && T > 0);
-  SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
-  hipStream_t st = (hipStream_t)stream;
-  BnFin fn{};
-  if (!fin) return launch_moments<false>(x, part, B, C, T, V, per_joint, fn, st);
-  const sgcn_bn_fold& f = fin->f;
-  SGCN_REQUIRE(fin->count && f.mean && f.invstd && f.scale && f.shift);
-  SGCN_REQUIRE((f.running_mean == nullptr) == (f.running_var == nullptr));
-  SGCN_REQUIRE(f.n_part == (per_joint ? T : T * V));
-  if (per_joint && V > kWave) {   // partials stored beyond wave 0: a separate finalize
-    const int rc = launch_moments<false>(x, part, B, C, T, V, per_joint, fn, st);
-    if (rc) return rc;
-    return sgcn_bn_finalize(part, B, C * V, T, V, f.gamma, f.beta, f.eps, f.momentum,
-                            f.running_mean, f.running_var, f.num_batches, f.mean, f.invstd,
-                            f.scale, f.shift, stream);
-  }
-  fn.f = f;
-  fn.f.part = part;
-  fn.count = fin->count;
-  fn.nf = per_joint ? V : 1;
-  fn.perm_V = per_joint ? V : 0;
-  return launch_moments<true>(x, part, B, C, T, V, per_joint, fn, st);
 }
 
 int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,

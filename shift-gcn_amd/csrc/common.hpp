@@ -8,7 +8,7 @@
 // Diagnostic builds (timing probes whose results are wrong; `make diag` only): any of
 // these macros marks the library, and sgcn_abi_version() then carries SGCN_ABI_DIAG_FLAG.
 #if defined(SGCN_PW_DIAG) || defined(SGCN_PW_STAMPS) || defined(SGCN_DIAG_X1B_BOUND) || \
-    defined(SGCN_DIAG_F2_BOUND) || defined(SGCN_DIAG_FIN)
+    defined(SGCN_DIAG_F2_BOUND)
 #define SGCN_DIAG_BUILD 1
 #else
 #define SGCN_DIAG_BUILD 0
@@ -299,122 +299,6 @@ __device__ __forceinline__ float3 bn_bwd_fold_channel(const sgcn_bn_bwd_fold& f,
   }
   __syncthreads();
   return fr;
-}
-
-// ---- producer-tail finalize (sgcn_bn_fin) ----------------------------------------------
-// Reference feature index of local feature f (perm_V > 0: per-joint f = d*V + v ->
-// v*D + d, the BatchNorm1d(V*C) order of shift_gcn.py:135-137).
-__device__ __forceinline__ int ref_feature(int f, int perm_V, int F) {
-  if (perm_V <= 0) return f;
-  const int D = F / perm_V;
-  const int d = f / perm_V, v = f - d * perm_V;
-  return v * D + d;
-}
-
-// Partials written / read at device coherence (sc1: through the XCD-private L2s), so the
-// workgroup that completes a channel reads every other XCD's partials without an
-// L2-wide write-back / invalidate.
-__device__ __forceinline__ void store_part(float2* p, float2 v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
-                     __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float2 load_part(const float2* p) {
-  return __builtin_bit_cast(
-      float2, __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<float2*>(p)),
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// Device form of sgcn_bn_fin: nf features per channel (1, or V per joint).
-struct BnFin {
-  sgcn_bn_fold f;
-  unsigned* count;
-  int nf, perm_V;
-};
-
-// Call from wave 0 (the only wave left: the others have exited) after its store_part()s
-// for channel c: true in the workgroup that is the B-th to finish channel c (its counter is
-// returned to zero). The waitcnt makes the partial stores complete before the count that
-// publishes them; only one wave per workgroup waits on the count's round trip.
-__device__ __forceinline__ bool channel_done(unsigned* count, int c, int B) {
-#if defined(SGCN_DIAG_FIN) && SGCN_DIAG_FIN >= 2
-  return false;   // diagnostic: no count (the finalize never runs: WRONG statistics)
-#endif
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  unsigned old = 0;
-  if ((threadIdx.x & 63) == 0)
-    old = __hip_atomic_fetch_add(count + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = __shfl(old, 0, kWave);
-  const bool last = old == (unsigned)B - 1;
-  if (last && (threadIdx.x & 63) == 0)
-    __hip_atomic_store(count + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return last;
-}
-
-// The finalize of channel c's nf features from their B partials (part[b][C*nf]), in
-// bn_finalize_kernel's order: sample b into partial sum (b mod 8) in increasing b (8 lanes
-// per feature), the eight merged 0..7 — bit-identical statistics. Call from wave 0 only.
-__device__ __forceinline__ void bn_fin_channel(const BnFin& fn, int c, int C, int B) {
-#if defined(SGCN_DIAG_FIN) && SGCN_DIAG_FIN == 1
-  return;         // diagnostic: counts only, no finalize work (WRONG statistics)
-#endif
-  const sgcn_bn_fold& f = fn.f;
-  const float2* __restrict__ part = (const float2*)f.part;
-  const int nf = fn.nf, F = C * nf;
-  const int lane = threadIdx.x & 63;
-  for (int i0 = 0; i0 < nf * 8; i0 += kWave) {   // 8 features per pass
-    const int i = i0 + lane, v = i >> 3, q = i & 7;
-    const int fe = c * nf + min(v, nf - 1);
-    double ax = 0.0, ay = 0.0, axx = 0.0;
-    int b = q;
-    for (; b + 56 < B; b += 64) {
-      float2 pv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) pv[u] = load_part(part + (size_t)(b + u * 8) * F + fe);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        ax += pv[u].x;
-        ay += pv[u].y;
-        axx += (double)pv[u].x * pv[u].x;
-      }
-    }
-    for (; b + 24 < B; b += 32) {
-      float2 pv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) pv[u] = load_part(part + (size_t)(b + u * 8) * F + fe);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        ax += pv[u].x;
-        ay += pv[u].y;
-        axx += (double)pv[u].x * pv[u].x;
-      }
-    }
-    for (; b < B; b += 8) {
-      const float2 pv = load_part(part + (size_t)b * F + fe);
-      ax += pv.x;
-      ay += pv.y;
-      axx += (double)pv.x * pv.x;
-    }
-    double sx = ax, sy = ay, sxx = axx;
-#pragma unroll
-    for (int k = 1; k < 8; ++k) {   // lanes q = 1..7 of this feature, in order
-      sx += __shfl(ax, lane + k, kWave);
-      sy += __shfl(ay, lane + k, kWave);
-      sxx += __shfl(axx, lane + k, kWave);
-    }
-    if (q == 0 && v < nf) {
-      const int rf = ref_feature(fe, fn.perm_V, F);
-      const float g = f.gamma ? f.gamma[rf] : 1.f;
-      const float be = f.beta ? f.beta[rf] : 0.f;
-      const BnCoef k = bn_train_coef(sx, sy, sxx, B, f.n_part, f.eps, g, be);
-      f.mean[fe] = k.mean;
-      f.invstd[fe] = k.invstd;
-      f.scale[fe] = k.scale;
-      f.shift[fe] = k.shift;
-      if (f.running_mean) bn_running_update(f.running_mean, f.running_var, rf, f.momentum, k);
-    }
-  }
-  if (c == 0 && lane == 0 && f.num_batches) *f.num_batches += 1;
 }
 
 }  // namespace sgcn

@@ -60,7 +60,6 @@ SIGNATURES = {
                         _I, _I, _I, _I, _I, _P]),
     "sgcn_moments_ws_bytes": (_Z, [_I, _I, _I, _I]),
     "sgcn_moments": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
-    "sgcn_moments_fin": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "sgcn_bn_finalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P,
                               _P]),
     "sgcn_bn_eval_coef": (_I, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P]),

@@ -216,14 +216,6 @@ def join_side(device):
 # ======================================================================================
 # Shift_gcn
 # ======================================================================================
-def _moments_bn(x, per_joint, B, F, n_part, bn):
-    """A BatchNorm2d's training statistics over x: the finalize in the moments launch's tail
-    (ops.moments_bn) or, with SGCN_TAIL_FINALIZE=0, a finalize its consumer may fold."""
-    if ops.TAIL_FINALIZE:
-        return ops.moments_bn(x, per_joint, bn)
-    return ops.bn_finalize(ops.moments(x, per_joint), B, F, n_part, bn, defer=True)
-
-
 class GcnSaved:
     __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
 
@@ -241,7 +233,7 @@ def gcn_forward(mod, x0, training, off=False):
         with down:
             ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
             if training:   # (folded into the gcn tail's apply below)
-                dst = _moments_bn(D0, False, B, Cout, T * V, bn)
+                dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn, defer=True)
             else:
                 dst = ops.bn_eval_coef(bn, Cout)
     cache = mod.__dict__.pop("_gather_cache", None)
@@ -255,7 +247,7 @@ def gcn_forward(mod, x0, training, off=False):
     # apply the joint rotation in their addressing (per_joint = 3)
     ops.pw_fwd(mod.Linear_weight, True, mod.Linear_bias, PV(xg), PV(Z), Cout, Cin, T, V)
     if training:
-        zst = ops.moments_bn(Z, 3, mod.bn)
+        zst = ops.bn_finalize(ops.moments(Z, 3), B, Cout * V, T, mod.bn, perm_V=V)
     else:
         zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
     if mod.has_down:
@@ -591,7 +583,7 @@ def convbn_core_forward(mod, x, training):
     Rc = _empty(B, Cout, To, V, like=x)
     ops.pw_fwd(conv.weight, False, conv.bias, PV(x, s_t), PV(Rc), Cout, Cin, To, V)
     if training:   # folded into the unit tail's apply
-        rst = _moments_bn(Rc, False, B, Cout, To * V, bn)
+        rst = ops.bn_finalize(ops.moments(Rc, False), B, Cout, To * V, bn, defer=True)
     else:
         rst = ops.bn_eval_coef(bn, Cout)
     s = ConvBnSaved()

@@ -824,68 +824,6 @@ def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True, defer=False):
     return st
 
 
-class BnFinStruct(ctypes.Structure):
-    """``sgcn_bn_fin`` (include/shiftgcn.h): a finalize run in its producer's tail."""
-    _fields_ = [("f", BnFoldStruct), ("count", ctypes.c_void_p)]
-
-
-# Training finalizes run in the tail of the launch that makes their partials (round 4,
-# sgcn_bn_fin; A/B knob SGCN_TAIL_FINALIZE): no finalize launch.
-TAIL_FINALIZE = int(__import__("os").environ.get("SGCN_TAIL_FINALIZE", "1"))
-_COUNT_N = 1 << 16
-_counters = {}
-
-
-def _fin_count(device, C):
-    """The zeroed per-channel counters of the current stream (each tail-finalize launch
-    leaves them zero; launches on one stream never overlap)."""
-    if C > _COUNT_N:
-        raise RuntimeError(f"{C} channels exceed the finalize counters ({_COUNT_N})")
-    s = torch.cuda.current_stream(device)
-    key = (device.index, s.cuda_stream)
-    t = _counters.get(key)
-    if t is None:
-        t = torch.zeros(_COUNT_N, device=device, dtype=torch.int32)
-        _counters[key] = t
-    return t
-
-
-def _bn_fin(bn, F, C, n_part, device, training):
-    """(BnStats, sgcn_bn_fin) of a tail finalize of ``bn`` over F features in C channels."""
-    st = BnStats(F, device)
-    track = training and bn.track_running_stats and bn.running_mean is not None
-    if track and bn.momentum is None:
-        raise NotImplementedError("BatchNorm momentum=None is not supported on the HIP path")
-    momentum = bn.momentum if bn.momentum is not None else 0.0
-    f = BnFoldStruct(None, _ptr(bn.weight), _ptr(bn.bias),
-                     _ptr(bn.running_mean) if track else None,
-                     _ptr(bn.running_var) if track else None,
-                     _ptr(bn.num_batches_tracked) if track else None, _ptr(st._mean),
-                     _ptr(st._invstd), _ptr(st._scale), _ptr(st._shift), int(n_part),
-                     float(bn.eps), float(momentum))
-    return st, BnFinStruct(f, _ptr(_fin_count(device, C)))
-
-
-def moments_bn(x, per_joint, bn, training=True):
-    """``bn_finalize(moments(x, per_joint), ...)``: the training statistics of ``bn`` over
-    x (BatchNorm2d, or per_joint=3 the per-joint BatchNorm1d(V*C) with perm_V = V), the
-    finalize in the moments launch's tail (sgcn_moments_fin) unless SGCN_TAIL_FINALIZE=0."""
-    B, C, T, V = x.shape
-    pj = V if per_joint else 0
-    F, n_part = C * (V if per_joint else 1), (T if per_joint else T * V)
-    if not TAIL_FINALIZE:
-        return bn_finalize(moments(x, per_joint), B, F, n_part, bn, perm_V=pj,
-                           training=training)
-    check_input(x, "input")
-    st, fin = _bn_fin(bn, F, C, n_part, x.device, training)
-    part = torch.empty((B * F * 2,), device=x.device, dtype=_F32)
-    with _timed("bn_stats", 0, 4 * x.numel(), x, "FIN " + _shp(x)):
-        rc = _lib.load().sgcn_moments_fin(_ptr(x), _ptr(part), B, C, T, V, int(per_joint),
-                                          ctypes.byref(fin), _stream(x))
-    _lib.check(rc, "sgcn_moments_fin")
-    return st
-
-
 def bn_eval_coef(bn, F, perm_V=0, device=None):
     st = BnStats(F, bn.running_mean.device, batch=False)
     with _timed("finalize", 0, 4 * 8 * F, bn.running_mean):
