@@ -1224,14 +1224,6 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
   SGCN_REQUIRE(x && part && T > 0);
   hipStream_t st = (hipStream_t)stream;
   SGCN_REQUIRE(per_joint == 0 || per_joint == 3);
-#ifdef SGCN_DIAG_ZST_SKIP
-  // diagnostic (`make diag` only): the per-joint statistics pass skipped — the bound of
-  // moving Shift_gcn.bn's moments into the gcn contraction epilogue (WRONG statistics)
-  if (per_joint == 3) return 0;
-#endif
-#ifdef SGCN_DIAG_ZS_EPI
-  if (per_joint == 3 && C <= 128) return 0;   // (made by the contraction epilogue instead)
-#endif
   {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
     const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);

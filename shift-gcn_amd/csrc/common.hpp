@@ -8,8 +8,7 @@
 // Diagnostic builds (timing probes whose results are wrong; `make diag` only): any of
 // these macros marks the library, and sgcn_abi_version() then carries SGCN_ABI_DIAG_FLAG.
 #if defined(SGCN_PW_DIAG) || defined(SGCN_PW_STAMPS) || defined(SGCN_DIAG_X1B_BOUND) || \
-    defined(SGCN_DIAG_F2_BOUND) || defined(SGCN_DIAG_ZST_SKIP) || \
-    defined(SGCN_DIAG_ZS_EPI)
+    defined(SGCN_DIAG_F2_BOUND)
 #define SGCN_DIAG_BUILD 1
 #else
 #define SGCN_DIAG_BUILD 0

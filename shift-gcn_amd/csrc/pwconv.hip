@@ -76,10 +76,6 @@ struct FwdArgs {
   const float* et;
   const float* er;
   unsigned er_bytes;
-#ifdef SGCN_DIAG_ZS_EPI
-  float2* zs;        // diagnostic: per (tile, row, joint) {sum, sum of squares}
-  float2* zs_head;   // ... of a plane's first columns inside the previous plane's last tile
-#endif
 };
 
 // relu(v * s + t + r) in this order, no contraction (the tshift_fwd_pre_kernel expression
@@ -226,7 +222,7 @@ __global__ void tshift_params_kernel(const float* __restrict__ xpos,
 // cost VALU per loaded element.
 // ------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM,
-          bool TSH = false, bool EPI = false, bool ZS = false>
+          bool TSH = false, bool EPI = false>
 __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   SGCN_CRIT_PRIO();
   static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
@@ -532,25 +528,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
             if constexpr (ACCUM) val += pf[k][q][0];
             bstore(yr, val, voff, soff);
           }
-#ifdef SGCN_DIAG_ZS_EPI
-          if constexpr (ZS) {
-            // diagnostic: the per-(row, joint) sums of the tile row (Shift_gcn.bn moments
-            // in the epilogue), split at the plane boundary
-            if (lane < V) {
-              const int b0 = p0 / N, jb = (b0 + 1) * N - p0;
-              float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
-              for (int j = lane; j < BN && p0 + j < P; j += V) {
-                const float v = smem[lr * BN + j] + bv;
-                if (j < jb) { s1a += v; s2a += v * v; }
-                else { s1b += v; s2b += v * v; }
-              }
-              const int w = v_s[lane];
-              p.zs[((size_t)(p0 / BN) * M + m0 + trow) * V + w] = make_float2(s1a, s2a);
-              if (jb < BN)
-                p.zs_head[((size_t)(b0 + 1) * M + m0 + trow) * V + w] = make_float2(s1b, s2b);
-            }
-          }
-#endif
         }
         __syncthreads();
       }
@@ -1140,13 +1117,6 @@ void launch_pwg(const FwdArgs& a, bool accum, hipStream_t st) {
 #define SGCN_PWG_AC(MS, XR, AM) \
   (accum ? SGCN_PWG(MS, XR, AM, true) : SGCN_PWG(MS, XR, AM, false))
 #define SGCN_PWG_AM(MS, XR) (amc ? SGCN_PWG_AC(MS, XR, true) : SGCN_PWG_AC(MS, XR, false))
-#ifdef SGCN_DIAG_ZS_EPI
-  if (a.zs) {
-    pwg_fwd_kernel<BM, BN, WM, WN, false, false, true, false, false, false, true>
-        <<<grid, 64 * WM * WN, 0, st>>>(a);
-    return;
-  }
-#endif
   if (mask) { if (xrot) SGCN_PWG_AM(true, true); else SGCN_PWG_AM(true, false); }
   else { if (xrot) SGCN_PWG_AM(false, true); else SGCN_PWG_AM(false, false); }
 #undef SGCN_PWG_AM
@@ -1342,20 +1312,6 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   // conv's read of the unit input is dropped by the range check, i.e. the most any fusion
   // sharing that read with the `down` conv (verdict r02, row f2) could save
   if (x_tstride == 2 && !ac) a.x_bytes = 0;
-#endif
-#ifdef SGCN_DIAG_ZS_EPI
-  // diagnostic (`make diag` only): the gcn contraction (bias, m-contiguous weights, plain
-  // planes) at M <= 128 also writes per-(tile, row, joint) sums to a scratch buffer, and
-  // sgcn_moments skips those layers' per-joint pass (statistics WRONG: timing only)
-  if (w_mcontig && bias && !rl && !ac && !mask && x_rsign == 0 && y_rsign == 0 && M > kSmallM &&
-      M <= 128 && T * V >= 256 && V <= 64) {
-    static float2* zbuf = nullptr;
-    const size_t ztile = ((size_t)B * T * V + 255) / 256 * M * V, zhead = (size_t)(B + 1) * M * V;
-    if (!zbuf && hipMalloc(&zbuf, (size_t)48 << 20 << 3) != hipSuccess) return SGCN_EINVAL;
-    if ((ztile + zhead) * sizeof(float2) > ((size_t)48 << 20 << 3)) return SGCN_EINVAL;
-    a.zs = zbuf;
-    a.zs_head = zbuf + ztile;
-  }
 #endif
   if (M <= kSmallM && SGCN_SMALLM && !mask && x_rsign == 0 && y_rsign == 0) {
     const unsigned grid = (unsigned)(((long long)B * T * V + 255) / 256);
