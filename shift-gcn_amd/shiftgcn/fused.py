@@ -204,10 +204,17 @@ def _pos_alloc(shift, off):
     return None if off else (ops.grad_like(shift.xpos), ops.grad_like(shift.ypos))
 
 
+# End of the backward (A/B knob SGCN_TAIL_MAIN, bits): 1 = the deferred finalizes launch on
+# the current stream BEFORE its wait for the side stream (the wait then finds the side's
+# last weight gradients done or nearly so); 2 = the chain's first unit (the last backward)
+# keeps its weight gradients on the current stream (linked_units)
+TAIL_MAIN = int(os.environ.get("SGCN_TAIL_MAIN", "0"))
+
+
 def join_side(device):
     """Launch the deferred side-stream finalizes, then make the current stream wait for
     every launch enqueued on the side stream."""
-    _flush_deferred(device)
+    _flush_deferred(device, side=not (TAIL_MAIN & 1))
     s = _SIDE.get(device)
     if s is not None:
         torch.cuda.current_stream(device).wait_stream(s)

@@ -221,8 +221,9 @@ def linked_units(units):
         for u, nxt in zip(units[:-1], units[1:]):
             u.__dict__["_gather_consumer"] = nxt.gcn1
             u.__dict__["_next_unit"] = nxt
-        for u in units:
-            u.__dict__["_off_path"] = True
+        for i, u in enumerate(units):
+            if i or not fused.TAIL_MAIN & 2:
+                u.__dict__["_off_path"] = True
         # every unit's tanh(Feature_Mask) + 1 in one launch (fused.prepare_masks)
         fused.prepare_masks([u.gcn1 for u in units])
         yield

@@ -38,6 +38,7 @@ t_all = time.perf_counter() - t_start
 print(f"host enqueue per step: {1e3 * sum(ts) / steps:.2f} ms (min {1e3 * min(ts):.2f}, "
       f"max {1e3 * max(ts):.2f}); wall per step incl. drain {1e3 * t_all / steps:.2f} ms; "
       f"enqueue total {1e3 * t_enq:.1f} ms")
+print("per step ms:", " ".join(f"{1e3 * t:.1f}" for t in ts))
 pr = cProfile.Profile()
 pr.enable()
 for _ in range(steps):
