@@ -143,6 +143,7 @@ class _OffPath:
                 t.record_stream(self.side)
         self.ev = torch.cuda.Event()
         self.ev.record(self.side)
+        _SIDE_SEQ[self.side] = _SIDE_SEQ.get(self.side, 0) + 1
         return False
 
     def wait(self):
@@ -208,16 +209,28 @@ def _pos_alloc(shift, off):
 # the current stream BEFORE its wait for the side stream (the wait then finds the side's
 # last weight gradients done or nearly so); 2 = the chain's first unit (the last backward)
 # keeps its weight gradients on the current stream (linked_units)
-TAIL_MAIN = int(os.environ.get("SGCN_TAIL_MAIN", "0"))
+TAIL_MAIN = int(os.environ.get("SGCN_TAIL_MAIN", "3"))
+
+
+# Side-stream launch groups enqueued (per side stream) and, per waiting stream, the count
+# it has already waited for: every linked unit queues a join, and a wait with nothing new
+# to wait for is one more barrier packet (≈ 5 µs) in front of the optimizer.
+_SIDE_SEQ = {}
+_JOINED = {}
 
 
 def join_side(device):
     """Launch the deferred side-stream finalizes, then make the current stream wait for
-    every launch enqueued on the side stream."""
+    every launch enqueued on the side stream (once: no wait when nothing new was enqueued
+    there since this stream's last join)."""
     _flush_deferred(device, side=not (TAIL_MAIN & 1))
     s = _SIDE.get(device)
     if s is not None:
-        torch.cuda.current_stream(device).wait_stream(s)
+        cur = torch.cuda.current_stream(device)
+        seq = _SIDE_SEQ.get(s, 0)
+        if _JOINED.get((cur, s)) != seq:
+            cur.wait_stream(s)
+            _JOINED[(cur, s)] = seq
 
 
 # ======================================================================================
