@@ -1150,6 +1150,10 @@ void launch_pwg_tsh(const FwdArgs& a, hipStream_t st) {
 #ifndef SGCN_PW_M128
 #define SGCN_PW_M128 2
 #endif
+// ... at M <= 64: 0 = 64 x 256 on 8 waves, 1 = 64 x 128 on 4 waves, 2 = 64 x 256 on 4 waves
+#ifndef SGCN_PW_M64
+#define SGCN_PW_M64 0
+#endif
 // ... at M > 128: 0 = 256 x 128 on 8 waves, 1 = 128 x 128 on 8 waves (two row blocks),
 // 2 = 256 x 64 on 4 waves
 #ifndef SGCN_PW_M256
@@ -1334,8 +1338,15 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
       if (ac) pw_fwd_smallm_kernel<false, true><<<grid, 256, 0, st>>>(a);
       else pw_fwd_smallm_kernel<false, false><<<grid, 256, 0, st>>>(a);
     }
-  } else if (M <= 64) launch_pwg<64, 256, 2, 4>(a, ac, st);
-  else if (M <= 128) {
+  } else if (M <= 64) {
+#if SGCN_PW_M64 == 1
+    launch_pwg<64, 128, 2, 2>(a, ac, st);
+#elif SGCN_PW_M64 == 2
+    launch_pwg<64, 256, 2, 2>(a, ac, st);
+#else
+    launch_pwg<64, 256, 2, 4>(a, ac, st);
+#endif
+  } else if (M <= 128) {
 #if SGCN_PW_M128 == 1
     launch_pwg<128, 128, 2, 2>(a, ac, st);
 #elif SGCN_PW_M128 == 2
