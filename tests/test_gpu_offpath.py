@@ -65,6 +65,24 @@ def test_side_stream_gradients_bit_identical():
             assert torch.equal(ba[n], bb[n]), n
 
 
+@pytest.mark.parametrize("tail", [0, 1, 2])
+def test_end_of_backward_variants_bit_identical(tail, monkeypatch):
+    """SGCN_TAIL_MAIN (the deferred finalizes / the last unit's weight gradients on the
+    main stream; the default is 3) and the once-per-backward join: same results."""
+    from shiftgcn import fused
+    monkeypatch.setattr(fused, "TAIL_MAIN", tail)
+    a = _run(1)
+    monkeypatch.setattr(fused, "TAIL_MAIN", 3)
+    b = _run(0)
+    for (la, ga, ba), (lb, gb, bb) in zip(a, b):
+        assert torch.equal(la, lb)
+        assert ga.keys() == gb.keys()
+        for n in ga:
+            assert torch.equal(ga[n], gb[n]), n
+        for n in ba:
+            assert torch.equal(ba[n], bb[n]), n
+
+
 def test_side_stream_gradients_are_taken_not_copied(monkeypatch):
     from shiftgcn import fused, ops
     dev = torch.device("cuda:0")
