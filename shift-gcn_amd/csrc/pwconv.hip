@@ -1144,22 +1144,6 @@ void launch_pwg_tsh(const FwdArgs& a, hipStream_t st) {
       <<<grid, 64 * WM * WN, 0, st>>>(a);
 }
 
-// forward / dX contraction tile at 64 < M <= 128 (A/B knob, compile time): 0 = 128 x 256 on
-// 8 waves, 1 = 128 x 128 on 4 waves, 2 = 128 x 128 on 8 waves (32 x 64 per wave: twice the
-// workgroups; pw_fwd class -2 %, step +0.25 % same-box, profiles/r04_tiles/)
-#ifndef SGCN_PW_M128
-#define SGCN_PW_M128 2
-#endif
-// ... at M <= 64: 0 = 64 x 256 on 8 waves, 1 = 64 x 128 on 4 waves, 2 = 64 x 256 on 4 waves
-#ifndef SGCN_PW_M64
-#define SGCN_PW_M64 0
-#endif
-// ... at M > 128: 0 = 256 x 128 on 8 waves, 1 = 128 x 128 on 8 waves (two row blocks),
-// 2 = 256 x 64 on 4 waves
-#ifndef SGCN_PW_M256
-#define SGCN_PW_M256 0
-#endif
-
 // byte extent of a plane operand: one past its last addressed element
 unsigned plane_bytes(long long bstride, long long cstride, int tstride, int B, int C, int T,
                      int V) {
@@ -1338,31 +1322,13 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
       if (ac) pw_fwd_smallm_kernel<false, true><<<grid, 256, 0, st>>>(a);
       else pw_fwd_smallm_kernel<false, false><<<grid, 256, 0, st>>>(a);
     }
-  } else if (M <= 64) {
-#if SGCN_PW_M64 == 1
-    launch_pwg<64, 128, 2, 2>(a, ac, st);
-#elif SGCN_PW_M64 == 2
-    launch_pwg<64, 256, 2, 2>(a, ac, st);
-#else
-    launch_pwg<64, 256, 2, 4>(a, ac, st);
-#endif
-  } else if (M <= 128) {
-#if SGCN_PW_M128 == 1
-    launch_pwg<128, 128, 2, 2>(a, ac, st);
-#elif SGCN_PW_M128 == 2
-    launch_pwg<128, 128, 4, 2>(a, ac, st);
-#else
-    launch_pwg<128, 256, 2, 4>(a, ac, st);
-#endif
-  } else {
-#if SGCN_PW_M256 == 1
-    launch_pwg<128, 128, 4, 2>(a, ac, st);
-#elif SGCN_PW_M256 == 2
-    launch_pwg<256, 64, 4, 1>(a, ac, st);
-#else
-    launch_pwg<256, 128, 4, 2>(a, ac, st);
-#endif
-  }
+  } else if (M <= 64) launch_pwg<64, 256, 2, 4>(a, ac, st);
+  // 64 < M <= 128: 128 x 128 tiles on 8 waves (32 x 64 per wave, twice the workgroups of
+  // the 128 x 256 tile): pw_fwd class -1.8 %, step +0.1..0.25 % same-box
+  // (profiles/r04_tiles/; 64 x 128 / 4-wave tiles at M <= 64 and 128 x 128 / 256 x 64
+  // tiles at M > 128 measured there too, not better)
+  else if (M <= 128) launch_pwg<128, 128, 4, 2>(a, ac, st);
+  else launch_pwg<256, 128, 4, 2>(a, ac, st);
   SGCN_LAUNCH_CHECK();
   return 0;
 }
