@@ -54,6 +54,23 @@ struct OutPlane {
   int rsign;
 };
 
+// Exact unsigned division by a runtime divisor d >= 1 for dividends n < 2^31: with
+// l = ceil(log2 d) and m = floor(2^32 (2^l - d) / d) + 1, n / d = (umulhi(m, n) + n) >> l
+// (the sum stays below 2^32 because n < 2^31 and umulhi(m, n) < n).
+struct FastDiv {
+  unsigned m, s;
+};
+inline FastDiv fast_div(unsigned d) {
+  unsigned l = 0;
+  while ((1ull << l) < d) ++l;
+  const unsigned long long m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return {(unsigned)m, l};
+}
+__device__ __forceinline__ int fdiv(int n, unsigned m, unsigned s) {
+  const unsigned u = (unsigned)n;
+  return (int)((__umulhi(m, u) + u) >> s);
+}
+
 struct FwdArgs {
   const float* A;   // weights
   int lda;
@@ -66,6 +83,9 @@ struct FwdArgs {
   OutPlane y;
   int M, K, T, V;
   int B;
+  // exact division by N = T*V and by V (FastDiv, set by fwd_divisors): the per-column
+  // (sample, t, v) decomposition without a ~35-instruction integer division each
+  unsigned divN_m, divN_s, divV_m, divV_s;
   // byte extents of the operands (buffer-descriptor ranges: an offset at or past the
   // extent loads 0 / drops the store) and epilogue flags
   unsigned x_bytes, y_bytes, a_bytes, mask_bytes;
@@ -77,6 +97,15 @@ struct FwdArgs {
   const float* er;
   unsigned er_bytes;
 };
+
+// the FastDiv constants of a.T * a.V and a.V (every FwdArgs launch sets them)
+inline void fwd_divisors(FwdArgs& a) {
+  const FastDiv n = fast_div((unsigned)(a.T * a.V)), v = fast_div((unsigned)a.V);
+  a.divN_m = n.m;
+  a.divN_s = n.s;
+  a.divV_m = v.m;
+  a.divV_s = v.s;
+}
 
 // relu(v * s + t + r) in this order, no contraction (the tshift_fwd_pre_kernel expression
 // of the same eval-mode Shift_gcn tail)
@@ -261,7 +290,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
 
   for (int i = tid; i < BM; i += NT) {
     bias_s[i] = (p.bias && m0 + i < M) ? p.bias[m0 + i] : 0.f;
-    rot_s[i] = pmod(p.y.rsign * (m0 + i), V);
+    rot_s[i] = p.y.rsign ? pmod(p.y.rsign * (m0 + i), V) : 0;
   }
 
   // ---- B column of this thread (fixed for the tile) ----
@@ -274,14 +303,15 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
     const int pc = p0 + nb;
     unsigned ycol = p.y_bytes;   // out of range: stores dropped
     if (pc < P) {
-      const int b = pc / N;
+      const int b = fdiv(pc, p.divN_m, p.divN_s);
       const int n = pc - b * N;
-      const int t = n / V;
+      const int t = fdiv(n, p.divV_m, p.divV_s);
       tt = t;
       vv = n - t * V;
-      xcol = (unsigned)(((long long)b * p.x.bstride + (long long)t * p.x.tstride * V +
-                         (XROT ? 0 : vv)) * 4);
-      ycol = (unsigned)(((long long)b * p.y.bstride + (long long)t * p.y.tstride * V) * 4);
+      // 32-bit offsets: every term is at most the operand's byte extent (< 2^32, host-checked)
+      xcol = ((unsigned)b * (unsigned)p.x.bstride + (unsigned)t * (unsigned)(p.x.tstride * V) +
+              (unsigned)(XROT ? 0 : vv)) * 4u;
+      ycol = ((unsigned)b * (unsigned)p.y.bstride + (unsigned)t * (unsigned)(p.y.tstride * V)) * 4u;
     }
     if (tid < BN) {
       ycol_s[nb] = ycol;
@@ -463,16 +493,20 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
     const int lr = wid + k * NW;
     return (lr >> 4) * (BM / WM) + i * 32 + 16 * h + (lr & 15);   // uniform
   };
-  auto voff_of = [&](int trow, int q) {
-    int vo = vq[q];
-    if (rotated) {   // shift_out rotation of the stored joint
-      vo += rot_s[trow];
-      vo = vo >= V ? vo - V : vo;
-    }
-    return vo;
-  };
-  auto epilogue = [&](auto relu_tag) {
+  // (ROT a compile-time branch: without the shift_out rotation a lane's store offsets are
+  // the same for every row, hoisted out of the row loops — the epilogue is most of the
+  // VALU work of a K <= 128 tile, which shares the issue with the fp32 MFMA)
+  auto epilogue = [&](auto relu_tag, auto rot_tag) {
     constexpr bool RELU = decltype(relu_tag)::value;
+    constexpr bool ROT = decltype(rot_tag)::value;
+    auto voff_of = [&](int trow, int q) {
+      int vo = vq[q];
+      if constexpr (ROT) {   // shift_out rotation of the stored joint
+        vo += rot_s[trow];
+        vo = vo >= V ? vo - V : vo;
+      }
+      return vo;
+    };
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -532,8 +566,13 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         __syncthreads();
       }
   };
-  if (p.relu) epilogue(std::true_type{});
-  else epilogue(std::false_type{});
+  if (rotated) {
+    if (p.relu) epilogue(std::true_type{}, std::true_type{});
+    else epilogue(std::false_type{}, std::true_type{});
+  } else {
+    if (p.relu) epilogue(std::true_type{}, std::false_type{});
+    else epilogue(std::false_type{}, std::false_type{});
+  }
 #ifdef SGCN_PW_STAMPS
   __builtin_amdgcn_s_waitcnt(0);   // stores issued and drained
 #endif
@@ -556,7 +595,12 @@ struct DwArgs {
   unsigned g_bytes, x_bytes, mask_bytes;   // buffer ranges (pw_dw3_kernel)
 };
 
-template <int BM, int BN, int WM, int WN, bool MASK>
+// PLAIN (no mask, no joint rotation, byte extents in g_bytes / x_bytes): full tiles take a
+// lane's position (sample, t, v) advanced incrementally from chunk to chunk and load through
+// buffer descriptors (one address add per load) instead of two integer divisions per chunk
+// and 64-bit pointer arithmetic per load (11 VALU per MFMA before: the VALU shares the
+// fp32 MFMA's issue); partial tiles keep the general path.
+template <int BM, int BN, int WM, int WN, bool MASK, bool PLAIN = false>
 __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
   constexpr int NT = 64 * WM * WN;
   // positions per chunk: a wave's 64 lanes read 64 consecutive positions (256 B) of one
@@ -602,7 +646,51 @@ __global__ __launch_bounds__(64 * WM * WN) void pw_dw_kernel(DwArgs p) {
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) rsum[i] = 0.f;
 
+  // PLAIN fast path state: the position of the next chunk to load
+  const bool fast = PLAIN && m0 + BM <= p.M && c0 + BN <= p.Nc;   // uniform
+  const auto gres = make_rsrc(p.g.ptr, PLAIN ? p.g_bytes : 0u);
+  const auto xres = make_rsrc(p.x.ptr, PLAIN ? p.x_bytes : 0u);
+  const unsigned grow = (unsigned)((m0 + r0) * gcs) * 4u, xrow = (unsigned)((c0 + r0) * xcs) * 4u;
+  const unsigned gstep = (unsigned)(RSTEP * gcs) * 4u, xstep = (unsigned)(RSTEP * xcs) * 4u;
+  const unsigned gbs = (unsigned)p.g.bstride, xbs = (unsigned)p.x.bstride;
+  const unsigned gts = (unsigned)(p.g.tstride * V), xts = (unsigned)(p.x.tstride * V);
+  const int t0 = kq / V, v0 = kq - (kq / V) * V, dt = BK / V, dv = BK - (BK / V) * V;
+  int fb = 0, fc = 0, fn = 0, ft = 0, fv = 0;
+  if (fast && q_begin < q_end) {
+    fb = q_begin / nchunk;
+    fc = q_begin - fb * nchunk;
+    fn = fc * BK + kq;
+    ft = fn / V;
+    fv = fn - ft * V;
+  }
+  auto load_fast = [&]() {
+    ncur = fn < N;
+    vcur = fv;
+    const unsigned gp = grow + ((unsigned)fb * gbs + (unsigned)ft * gts + (unsigned)fv) * 4u;
+    const unsigned xp = xrow + ((unsigned)fb * xbs + (unsigned)ft * xts + (unsigned)fv) * 4u;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) ra[i] = bload(gres, gp + (unsigned)i * gstep, 0);
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) rb[i] = bload(xres, xp + (unsigned)i * xstep, 0);
+    // next chunk: BK positions on, or the next sample's first
+    if (++fc == nchunk) {
+      fc = 0;
+      ++fb;
+      fn = kq;
+      ft = t0;
+      fv = v0;
+    } else {
+      fn += BK;
+      ft += dt;
+      fv += dv;
+      if (fv >= V) { fv -= V; ++ft; }
+    }
+  };
   auto load_stage = [&](int q) {
+    if (fast) {
+      load_fast();
+      return;
+    }
     const int b = q / nchunk;
     const int n = (q - b * nchunk) * BK + kq;
     const bool nvalid = n < N;
@@ -1256,7 +1344,13 @@ int dwc_splits(int M, long long P) {
 
 // pw_dw3 measured faster from 128x128 contractions up (tools/bench/pwbench: l5/l6 tcn,
 // l9 tcn/gcn), equal or slower on the 64-wide masked/rotated ones
-bool use_dw3(int M, int Nc) { return (long long)M * Nc >= 128 * 128; }
+#ifndef SGCN_DW_PLAIN
+#define SGCN_DW_PLAIN 1   // A/B knob: the plain-operand fast path of pw_dw_kernel
+#endif
+#ifndef SGCN_DW3_MIN
+#define SGCN_DW3_MIN (128 * 128)
+#endif
+bool use_dw3(int M, int Nc) { return (long long)M * Nc >= SGCN_DW3_MIN; }
 
 }  // namespace
 }  // namespace sgcn
@@ -1294,6 +1388,7 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   a.T = T;
   a.V = V;
   a.B = B;
+  fwd_divisors(a);
   hipStream_t st = (hipStream_t)stream;
   const bool rl = relu != 0, ac = accumulate != 0;
   a.x_bytes = plane_bytes(x_bstride, x_cstride, x_tstride, B, K, T, V);
@@ -1360,6 +1455,7 @@ int sgcn_pw_fwd_bn_res(const float* w, int w_mcontig, const float* bias, const f
   a.T = T;
   a.V = V;
   a.B = B;
+  fwd_divisors(a);
   a.x_bytes = plane_bytes(x_bstride, x_cstride, 1, B, K, T, V);
   a.y_bytes = plane_bytes(y_bstride, y_cstride, 1, B, M, T, V);
   a.a_bytes = (unsigned)((long long)M * K * 4);
@@ -1412,6 +1508,7 @@ int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long l
   a.T = T;
   a.V = V;
   a.B = B;
+  fwd_divisors(a);
   a.x_bytes = plane_bytes(x_bstride, x_cstride, 1, B, K, T, V);
   a.y_bytes = plane_bytes(y_bstride, y_cstride, 1, B, M, T, V);
   a.a_bytes = (unsigned)((long long)M * K * 4);
@@ -1487,9 +1584,21 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
     a.bslab = dbias ? (float*)ws + (size_t)S * M * Nc : nullptr;
     a.chunks_per_split = (total + S - 1) / S;
     dim3 grid(tiles, S);
+    // the buffer-descriptor fast path: plain operands whose byte extents fit 32 bits
+    const long long ge = (long long)(B - 1) * g_bstride + (long long)M * g_cstride +
+                         (long long)T * g_tstride * V;
+    const long long xe = (long long)(B - 1) * x_bstride + (long long)Nc * x_cstride +
+                         (long long)T * x_tstride * V;
+    const bool plain = !mask && g_rsign == 0 && x_rsign == 0 && SGCN_DW_PLAIN &&
+                       ge < (1LL << 29) && xe < (1LL << 29);
+    if (plain) {
+      a.g_bytes = plane_bytes(g_bstride, g_cstride, g_tstride, B, M, T, V);
+      a.x_bytes = plane_bytes(x_bstride, x_cstride, x_tstride, B, Nc, T, V);
+    }
 #define SGCN_DW(BM_, BN_)                                                                    \
     (mask ? pw_dw_kernel<BM_, BN_, BM_ / 32, 2, true>                                           \
                 <<<grid, 64 * (BM_ / 32) * 2, (size_t)V * BN_ * sizeof(float), st>>>(a)       \
+          : plain ? pw_dw_kernel<BM_, BN_, BM_ / 32, 2, false, true><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a) \
           : pw_dw_kernel<BM_, BN_, BM_ / 32, 2, false><<<grid, 64 * (BM_ / 32) * 2, 0, st>>>(a))
     if (bm == 128 && bn == 128) SGCN_DW(128, 128);
     else if (bm == 128) SGCN_DW(128, 64);

@@ -121,6 +121,7 @@ int main(int argc, char** argv) {
       a.mask = s.mask ? mask : nullptr;
       a.y = {y2, s.M * N, N, 1, s.rot ? 1 : 0};
       a.M = s.M; a.K = s.K; a.T = s.T; a.V = s.V; a.B = s.B;
+      fwd_divisors(a);
       auto L = [&]() {
         sgcn_pw_fwd(w, 0, nullptr, x, s.K * N, N, 1, s.rot ? 1 : 0, s.mask ? mask : nullptr,
                     y2, s.M * N, N, 1, s.rot ? 1 : 0, 0, 0, s.B, s.M, s.K, s.T, s.V, st);
