@@ -332,6 +332,10 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
                              : (unsigned)(((m0 + am) * lda + ak) * 4);
   // per-i uniform step of the A element: AMC -> k += NT/BM, else m += NT/BK
   const unsigned astep = AMC ? (unsigned)((NT / BM) * lda * 4) : (unsigned)((NT / BK) * lda * 4);
+  // k-contiguous A: a k past K would alias the next row, so the lane's stage loads go out
+  // of the descriptor range (0) when k0 + ak >= K (one compare + select per stage instead
+  // of masking every loaded value)
+  const int kspan = K - ak;
 
   float ra[A_PER], rb[B_PER], rm[MASK ? B_PER : 1];
   float rq[TSH ? B_PER : 1][TSH ? 3 : 1];   // TSH: taps q21, q12, q22 (q11 in rb)
@@ -371,7 +375,8 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
     const unsigned ak0 = AMC ? (unsigned)(k0 * lda * 4) : (unsigned)(k0 * 4);
 #pragma unroll
     for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i)
-      ra[i] = bload_pol<SGCN_PW_APOL>(ar, avoff, ak0 + (unsigned)i * astep);
+      ra[i] = bload_pol<SGCN_PW_APOL>(ar, AMC ? avoff : (k0 < kspan ? avoff : p.a_bytes),
+                                      ak0 + (unsigned)i * astep);
   };
   const int T = p.T;
   auto store_stage = [&](int buf, int k0) {
@@ -393,10 +398,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         if (p.xs) bstore(xsr, val, colok ? xcol : p.x_bytes, (unsigned)row * xcs4);
       }
       Bs[buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
-    }
-    if (!AMC && k0 + BK > K) {   // k-contiguous A: a k past K aliases the next row
-#pragma unroll
-      for (int i = 0; i < A_PER; ++i) ra[i] = keep(ra[i], k0 + ak < K);
     }
 #pragma unroll
     for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i) {
