@@ -536,7 +536,6 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
                     g.x1 >= -1 && g.x1 <= 0;
   const auto orr = make_rsrc(out + ooff, (unsigned)n * 4u);
   const auto ogr = make_rsrc(GOUT ? og + ooff : out + ooff, GOUT ? (unsigned)n * 4u : 0u);
-  const int nfull = n / NTJ;   // elements e < nfull are inside the plane for every lane
   const int nval = own ? (n - tid + NTJ - 1) / NTJ : 0;   // this lane's elements e < nval
   float v[STATS ? LPT : 1];
   auto emit = [&](int e, float val) {
@@ -558,9 +557,9 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     const int lstep = GR * stride * WP;
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
-      // (a lane that owns no element, tid >= NTJ, would start one row group past the plane)
-      const bool tail = e >= nfull || !own;
-      const int la = tail ? min(la0 + e * lstep, lmax) : la0 + e * lstep;
+      // (a lane that owns no element, tid >= NTJ, would start one row group past the plane;
+      // an in-plane element's base never exceeds lmax, so one min clamps only the others)
+      const int la = min(la0 + e * lstep, lmax);
       emit(e, blend(pl[la], pl[la + 1], pl[la + WP], pl[la + WP + 1], g.dx, g.dy));
     }
   } else {
@@ -1114,7 +1113,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
       const bool tail = e >= nfull;
-      const int lt = tail ? min(l0, lmax) : l0;
+      const int lt = min(l0, lmax);   // (an in-plane element's base never exceeds lmax)
       const int la = lt + kq, lg = lt + kg;
       elem(e, tail, lds[la], lds[la + 1], lds[la + WP], lds[la + WP + 1], lds[lg + WP + 1],
            lds[lg + WP], lds[lg + 1], lds[lg]);
