@@ -9,7 +9,10 @@ Inputs are resident in HBM before the timed region. Weak scaling: 64 clips per G
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config ntu|mp|ens] [--graph 0|1]
 --config ens: BASELINE config 4 instead (4-stream MediaPipe ensemble inference, bs=256,
 eval mode, one hipGraph per batch): windows/s, its own JSON line.
-N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+N>1: `python bench.py --gpus N` starts N ranks itself (one process per GPU, through
+torch.distributed.run as a child process, before anything touches a GPU), or run it under
+an explicit launcher: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N;
+a launcher's WORLD_SIZE that differs from --gpus is an error (exit 2).
 
 Prints ONE JSON line on rank 0 (value = whole-job clips/s), with:
   roofline     — dominant kernel class of the timed region, achieved algorithmic
@@ -208,9 +211,53 @@ def cpu_baseline(cfg, seconds_budget=30.0):
         mo.Shift.function = prev_fn
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, n, port):
+    """The child command that runs this benchmark on ``n`` ranks of this node (one process
+    per GPU, rendezvous on 127.0.0.1): the same arguments, under torch.distributed.run."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, env):
+    """World size this process must run at: ``--gpus`` when no launcher set WORLD_SIZE
+    (None = start the ranks first), else the launcher's, which must equal ``--gpus``."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return None if gpus > 1 else 1
+    if int(ws) != gpus:
+        raise SystemExit(2)
+    return int(ws)
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        raise SystemExit(2)
+    try:
+        world = check_world(args.gpus, os.environ)
+    except SystemExit:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE="
+              f"{os.environ.get('WORLD_SIZE')} ranks", file=sys.stderr)
+        raise
+    if world is None:
+        # --gpus N without a launcher: start the N ranks as a child process (nothing in this
+        # process has touched a GPU), relay their output, exit with their status
+        import subprocess
+        have = torch.cuda.device_count()   # (does not initialise a device on this image)
+        if have < args.gpus and os.environ.get("SGCN_BENCH_SAME_DEVICE") != "1":
+            print(f"bench.py: --gpus {args.gpus} but {have} GPUs are visible", file=sys.stderr)
+            raise SystemExit(2)
+        cmd = launch_command(sys.argv[1:], args.gpus, _free_port())
+        raise SystemExit(subprocess.call(cmd))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
@@ -281,23 +328,6 @@ def main():
             return train.train_step(model, opt, xb, yb, grad_sync=sync)
         return train.train_step(model, opt, x, label, grad_sync=sync)
 
-    main_ctx = None
-    if os.environ.get("SGCN_MAIN_CUS_EXCLUDE_SIDE") == "1":
-        # A/B knob: the whole step on a CU-masked stream over the CUs the (CU-masked) side
-        # stream does not use
-        import ctypes
-
-        from shiftgcn import _lib, fused
-        total = ctypes.c_int(0)
-        _lib.check(_lib.load().sgcn_device_cu_count(dev.index or 0, ctypes.byref(total)),
-                   "sgcn_device_cu_count")
-        side = set(fused.cu_mask_bits(total.value, fused.SIDE_CUS, fused.SIDE_CU_PATTERN)
-                   if fused.SIDE_CUS > 0 else [])
-        ms = fused.masked_stream(dev, [c for c in range(total.value) if c not in side])
-        ms.wait_stream(torch.cuda.current_stream(dev))
-        main_ctx = torch.cuda.stream(ms)
-        main_ctx.__enter__()
-
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -324,10 +354,9 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rank_ms = [round(1000.0 * elapsed / args.steps, 3)]
     if distributed:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, rank_ms = _max_over_ranks(elapsed, dev, world, args.steps)
 
     clips = args.batch * world * args.steps
     value = clips / elapsed
@@ -404,7 +433,7 @@ def main():
                             "; roofline/breakdown steps: serialized (each class timed alone)"}
 
     cpu = None
-    if args.cpu_baseline and rank == 0 and world == 1:
+    if args.cpu_baseline and rank == 0:   # after the timed region (the other ranks wait)
         cpu = cpu_baseline(args.config)
 
     if rank == 0:
@@ -428,13 +457,36 @@ def main():
             "config": {"workload": f"{args.config.upper()} Shift-GCN training step "
                                    f"(fwd+CE+bwd+SGD), x=({args.batch},3,{T},{V},{M}) per GPU",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                       "parallelism": f"dp{world}", "hipgraph": bool(args.graph)},
+                       "parallelism": f"dp{world}", "hipgraph": bool(args.graph),
+                       **_ranks_info(distributed, world, rank_ms)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if distributed:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def _max_over_ranks(elapsed, dev, world, steps):
+    """(max over ranks of the timed region, every rank's ms per step in rank order)."""
+    t = torch.zeros(world, device=dev, dtype=torch.float64)
+    t[dist.get_rank()] = elapsed
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)   # each rank fills its own slot
+    per = t.cpu().tolist()
+    return max(per), [round(1000.0 * e / steps, 3) for e in per]
+
+
+def _ranks_info(distributed, world, rank_ms):
+    """What ran: the process group's size and backend as torch.distributed reports them
+    (1 / "none" without one) and each rank's timed ms per step."""
+    if distributed:
+        ws, be = dist.get_world_size(), str(dist.get_backend())
+        if ws != world:
+            raise RuntimeError(f"process group has {ws} ranks, WORLD_SIZE={world}")
+    else:
+        ws, be = 1, "none"
+    return {"world_size": ws, "backend": be, "rank_ms_per_step": rank_ms}
 
 
 def _roofline(summ, n_iters, value_per_gpu, gflop_per_unit):
@@ -522,10 +574,9 @@ def bench_ensemble(args, dev, rank, world, distributed):
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rank_ms = [round(1000.0 * elapsed / args.steps, 3)]
     if distributed:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, rank_ms = _max_over_ranks(elapsed, dev, world, args.steps)
     value = batch * world * args.steps / elapsed
     roof = None
     if args.roofline and rank == 0:
@@ -550,7 +601,7 @@ def bench_ensemble(args, dev, rank, world, distributed):
         roof["traffic"] = None if traffic is None else round(traffic)
         roof["traffic_unit"] = "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
         roof["traffic_source"] = tsrc or None
-    cpu = cpu_baseline_ensemble() if (args.cpu_baseline and rank == 0 and world == 1) else None
+    cpu = cpu_baseline_ensemble() if (args.cpu_baseline and rank == 0) else None
     if rank == 0:
         print(json.dumps({
             "metric": "ensemble windows/sec, MediaPipe 4-stream (3,300,33,1) bs=256 inference",
@@ -562,9 +613,11 @@ def bench_ensemble(args, dev, rank, world, distributed):
             "config": {"workload": f"ENS 4-stream eval forward + score fusion, "
                                    f"x=({batch},3,300,33,1) per GPU",
                        "global_batch": batch * world, "per_gpu_batch": batch,
-                       "parallelism": f"replicas{world}", "hipgraph": bool(args.graph_ens)},
+                       "parallelism": f"replicas{world}", "hipgraph": bool(args.graph_ens),
+                       **_ranks_info(distributed, world, rank_ms)},
             "roofline": roof, "cpu_baseline": cpu}), flush=True)
     if distributed:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 21
+#define SGCN_ABI_VERSION 22
 /* Set in sgcn_abi_version()'s value by a diagnostic build (SGCN_PW_DIAG, SGCN_PW_STAMPS,
  * SGCN_DIAG_*: timing probes whose results are WRONG, `make diag` only); the Python loader
  * refuses such a library. */
@@ -35,50 +35,12 @@ extern "C" {
  * d_part; NULL when the Shift_gcn has none); sgcn_sgd_step (the optimizer update).
  * 21: sgcn_sgd_step's per-tensor gradient scale (flags bit 1 + the float in bits 32-63: the
  * data-parallel reduction's 1/world applied inside the update, written back to the grad);
- * sgcn_pw_fwd_bn_res (the inference Shift_gcn tail in the contraction epilogue). */
+ * 22: the round-4 measured-and-rejected variants are gone (the folded BatchNorm finalizes
+ * sgcn_bn_fold / sgcn_bn_bwd_fold and their consumers sgcn_tshift_fwd_fold,
+ * sgcn_bn_apply_fold, sgcn_tshift_bwd_bnin_fold, sgcn_bn_bwd_apply_fold; the inference
+ * epilogue sgcn_pw_fwd_bn_res; the CU-masked streams), and so are the fold structs in the
+ * default kernels' argument lists. */
 int sgcn_abi_version(void);
-
-/* A training-mode per-channel BatchNorm finalize FOLDED into its first consumer (round 4):
- * the consumer's (sample, channel) plane workgroups each merge their channel's B partials
- * (sgcn_moments / sgcn_tshift_fwd plane_stats layout, (B*C) float2 {mean, M2} over n_part
- * elements each) in sgcn_bn_finalize's order, so the coefficients are bit-identical to
- * that kernel's; the workgroup of sample 0 writes mean/invstd/scale/shift (C each) and
- * updates the running statistics (gamma/beta NULL = 1/0; running_* NULL = not tracked;
- * num_batches += 1 once). Consumers: sgcn_tshift_fwd_fold, sgcn_bn_apply_fold. */
-typedef struct sgcn_bn_fold {
-  const void* part;
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  long long* num_batches;
-  float* mean;
-  float* invstd;
-  float* scale;
-  float* shift;
-  int n_part;
-  float eps;
-  float momentum;
-} sgcn_bn_fold;
-
-/* A per-channel BatchNorm BACKWARD finalize folded into its consumer (round 4): the
- * consumer's plane workgroups merge part ((B*C) float2 {sum g, sum g*xhat}, the
- * sgcn_bn_bwd_reduce / sgcn_gcn_dx_finish / sgcn_tshift_bwd bn_part layout) in
- * sgcn_bn_bwd_finalize's order into that kernel's coefficients; the workgroup of sample 0
- * writes coef[3][C] and dgamma/dbeta (NULL = not written; accumulate 0). mean/invstd: the
- * BatchNorm's forward statistics; batch_stats 0 = a running-statistics BatchNorm.
- * Consumers: sgcn_tshift_bwd_bnin_fold, sgcn_bn_bwd_apply_fold. */
-typedef struct sgcn_bn_bwd_fold {
-  const void* part;
-  const float* mean;
-  const float* invstd;
-  const float* gamma;
-  float* dgamma;
-  float* dbeta;
-  float* coef;
-  double n_total;
-  int batch_stats;
-} sgcn_bn_bwd_fold;
 
 /* ------------------------------------------------------------------------------------
  * Temporal shift
@@ -139,14 +101,6 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
                          const float* in, const float* xpos, const float* ypos, float* gin,
                          float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                          int W, int ypos_is_raw, void* stream);
-/* sgcn_tshift_bwd_bnin with bn2's backward finalize folded in (`fold`, coef NULL; fold->coef
- * is written). Same plane limits. */
-int sgcn_tshift_bwd_bnin_fold(const float* dy, const float* y, const float* s,
-                              const float* coef, const sgcn_bn_bwd_fold* fold, const float* in,
-                              const float* xpos, const float* ypos, float* gin, float* gx,
-                              float* gy, void* ws, size_t ws_bytes, int B, int C, int H, int W,
-                              int ypos_is_raw, void* stream);
-
 /* Workspace bytes for sgcn_tshift_bwd (B*C float2 plane partials). */
 size_t sgcn_tshift_bwd_ws_bytes(int B, int C);
 
@@ -241,21 +195,6 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
                 int y_tstride, int y_rsign, int relu, int accumulate, int B, int M, int K,
                 int T, int V, void* stream);
 
-/* Inference Shift_gcn in ONE launch (shift_gcn.py:131-141, BatchNorms in eval mode; round 4):
- *   H[b][m][out(n,m)] = relu( (sum_k A[m][k] X(b,k,n) + bias[m]) * out_scale[m*V + v'] +
- *                             out_shift[m*V + v'] + res[b][m][out(n,m)] ),
- * v' = the stored (shift_out-rotated by y_rsign) joint, res with y's layout (the identity
- * down = the unit input, or the down conv's output with its BatchNorm folded into the conv
- * weights). out_scale/out_shift: BatchNorm1d(V*C_out)'s eval apply coefficients in the
- * natural [channel][joint] order. A as sgcn_pw_fwd; x plain (the gathered, masked gcn
- * input); the product in the same order as sgcn_tshift_fwd_pre's staging, so H is what that
- * kernel formed in registers. M, K <= 256. */
-int sgcn_pw_fwd_bn_res(const float* w, int w_mcontig, const float* bias, const float* x,
-                       long long x_bstride, long long x_cstride, const float* out_scale,
-                       const float* out_shift, const float* res, float* y,
-                       long long y_bstride, long long y_cstride, int y_rsign, int B, int M,
-                       int K, int T, int V, void* stream);
-
 /* Shift_tcn's shift_in fused into its temporal_linear (shift_gcn.py:66-70):
  *   Y[b][m][n] = act( sum_k w[m*K + k] * S_k(b, n) + bias[m] ),
  *   S_k = shift_k(in_scale[k] * X[b][k] + in_shift[k])   (stride-1 temporal shift,
@@ -314,14 +253,6 @@ int sgcn_moments(const float* x, float* part, int B, int C, int T, int V, int pe
  * order); updates running_mean/var (momentum, unbiased var) and num_batches (+1) when
  * non-NULL, in the reference feature order (perm_V > 0: per-joint mapping). */
 
-/* sgcn_tshift_fwd with the input affine (in_scale/in_shift) of a folded finalize: `fold`
- * (NULL = no affine) writes fold->mean/invstd/scale/shift (C). Planes the padded LDS
- * kernel does not take run the finalize as its own launch first (same values). */
-int sgcn_tshift_fwd_fold(const float* in, float* out, const float* xpos, const float* ypos,
-                         const sgcn_bn_fold* fold, float* plane_stats, int B, int C, int H,
-                         int W, int stride, int ypos_is_raw, void* stream);
-
-
 int sgcn_bn_finalize(const float* part, int B, int F, int n_part, int perm_V,
                      const float* gamma, const float* beta, float eps, float momentum,
                      float* running_mean, float* running_var, long long* num_batches,
@@ -343,14 +274,6 @@ int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int pe
                   const float* r, const float* rscale, const float* rshift, int relu,
                   float* y, float* y_stats, const float* gather_m, float* y_gathered, int B,
                   int C, int T, int V, void* stream);
-/* sgcn_bn_apply with folded finalizes: `fold` (per_joint == 0 only) supplies scale/shift,
- * `rfold` (with r; rscale/rshift NULL) the residual's; either NULL = as sgcn_bn_apply. */
-int sgcn_bn_apply_fold(const float* x, const float* scale, const float* shift, int per_joint,
-                       const sgcn_bn_fold* fold, const float* r, const float* rscale,
-                       const float* rshift, const sgcn_bn_fold* rfold, int relu, float* y,
-                       float* y_stats, const float* gather_m, float* y_gathered, int B, int C,
-                       int T, int V, void* stream);
-
 /* Backward partials: g = dy * (relu ? y > 0 : 1); part[b][f] = {sum g, sum g*xhat};
  * rpart[b][c] likewise for a BatchNorm2d residual input r (NULL = none).
  * dy_coef (optional, [3][C], requires relu): dy is replaced by k1[c]*dy + k2[c]*y + k3[c],
@@ -386,13 +309,6 @@ int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
                       const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
                       void* stream);
-/* sgcn_bn_bwd_apply with folded backward finalizes: `fold` (per_joint 0; coef ignored) and
- * `rfold` (with r and dr; rcoef NULL); either NULL = as sgcn_bn_bwd_apply. */
-int sgcn_bn_bwd_apply_fold(const float* dy, const float* y, int relu, const float* x,
-                           const float* coef, int per_joint, const sgcn_bn_bwd_fold* fold,
-                           const float* r, const float* rcoef, const sgcn_bn_bwd_fold* rfold,
-                           const float* dy_coef, float* dx, float* dr, int B, int C, int T,
-                           int V, void* stream);
 
 /* m = tanh(Feature_Mask) + 1 (shift_gcn.py:129); n = V*C. */
 int sgcn_mask_prep(const float* mask, float* m, int n, void* stream);
@@ -518,16 +434,6 @@ int sgcn_mask_prep_many(const float* const* mask, float* const* m, const int* co
 int sgcn_mask_grad_finalize_many(const float* const* part, const float* const* mask,
                                  float* const* dmask, const int* B, const int* C,
                                  const int* V, int n, void* stream);
-
-/* ------------------------------------------------------------------------------------
- * CU-masked streams (hipExtStreamCreateWithCUMask), round 4: the weight-gradient side
- * stream confined to a subset of the CUs. mask: `words` uint32, bit i = CU i of the
- * device's multiProcessorCount CUs.
- * ------------------------------------------------------------------------------------ */
-int sgcn_device_cu_count(int device, int* count);
-int sgcn_stream_create_cu_mask(const unsigned* mask, int words, void** stream);
-int sgcn_stream_get_cu_mask(void* stream, unsigned* mask, int words);
-int sgcn_stream_destroy(void* stream);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -386,8 +386,7 @@ __global__ __launch_bounds__(NT) void bn_apply_ja_kernel(
     const float* __restrict__ shift, const float* __restrict__ r,
     const float* __restrict__ rscale, const float* __restrict__ rshift,
     float* __restrict__ y, float2* __restrict__ ystats, const float* __restrict__ gm,
-    float* __restrict__ yg, int C, int T, int V, const sgcn_bn_fold fm = sgcn_bn_fold{},
-    const sgcn_bn_fold fr = sgcn_bn_fold{}) {
+    float* __restrict__ yg, int C, int T, int V) {
   SGCN_CRIT_PRIO();
   constexpr bool OUT_STATS = OUTX == 1, OUT_G = OUTX == 2;
   __shared__ float red[2 * NT / 64];
@@ -415,28 +414,9 @@ __global__ __launch_bounds__(NT) void bn_apply_ja_kernel(
       for (int e = 0; e < LPT; ++e) rv[e] = bload(rr, vo + e * vstep, 0);
     }
   }
-  // folded finalizes (sgcn_bn_fold, uniform per launch): the per-channel coefficients are
-  // merged from the batch partials here, while the plane's loads are in flight
-  float sc, sh;
-  if (!PER_JOINT && fm.part) {
-    const float2 k = bn_fold_channel(fm, c, C, plane / C, (int)gridDim.x / C);
-    sc = k.x;
-    sh = k.y;
-  } else {
-    sc = PER_JOINT ? scale[c * V + w] : scale[c];
-    sh = PER_JOINT ? shift[c * V + w] : shift[c];
-  }
-  float rsc = 1.f, rsh = 0.f;
-  if (RES == 2) {
-    if (fr.part) {
-      const float2 k = bn_fold_channel(fr, c, C, plane / C, (int)gridDim.x / C);
-      rsc = k.x;
-      rsh = k.y;
-    } else {
-      rsc = rscale[c];
-      rsh = rshift[c];
-    }
-  }
+  const float sc = PER_JOINT ? scale[c * V + w] : scale[c];
+  const float sh = PER_JOINT ? shift[c * V + w] : shift[c];
+  const float rsc = RES == 2 ? rscale[c] : 1.f, rsh = RES == 2 ? rshift[c] : 0.f;
   const float gmu = OUT_G ? gm[wz * C + c] : 0.f;
   const auto yr = make_rsrc(y + off, pb);
   const auto ygr = make_rsrc(OUT_G ? yg + off : y + off, OUT_G ? pb : 0u);
@@ -832,8 +812,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_ja_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ coef, int F, const float* __restrict__ r,
     const float* __restrict__ rcoef, int RF, const float* __restrict__ dyc,
-    float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V,
-    const sgcn_bn_bwd_fold fm = sgcn_bn_bwd_fold{}, const sgcn_bn_bwd_fold fr = sgcn_bn_bwd_fold{}) {
+    float* __restrict__ dx, float* __restrict__ dr, int C, int T, int V) {
   SGCN_CRIT_PRIO();
   static_assert(PJM == 0 || PJM == 3, "per-channel, or per-joint gathered (ZU)");
   constexpr bool PER_JOINT = PJM == 3;
@@ -869,31 +848,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_ja_kernel(
     }
   }
   const int f = PER_JOINT ? c * V + w : c;
-  float k1, k2, k3;
-  if (!PER_JOINT && fm.part) {   // folded backward finalizes (uniform per launch)
-    const float3 k = bn_bwd_fold_channel(fm, c, C, plane / C, (int)gridDim.x / C);
-    k1 = k.x;
-    k2 = k.y;
-    k3 = k.z;
-  } else {
-    k1 = coef[f];
-    k2 = coef[F + f];
-    k3 = coef[2 * F + f];
-  }
+  const float k1 = coef[f], k2 = coef[F + f], k3 = coef[2 * F + f];
   float d1 = 1.f, d2 = 0.f, d3 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
   if (DYT) { d1 = dyc[c]; d2 = dyc[C + c]; d3 = dyc[2 * C + c]; }
-  if (RES == 2) {
-    if (fr.part) {
-      const float3 k = bn_bwd_fold_channel(fr, c, C, plane / C, (int)gridDim.x / C);
-      q1 = k.x;
-      q2 = k.y;
-      q3 = k.z;
-    } else {
-      q1 = rcoef[c];
-      q2 = rcoef[RF + c];
-      q3 = rcoef[2 * RF + c];
-    }
-  }
+  if (RES == 2) { q1 = rcoef[c]; q2 = rcoef[RF + c]; q3 = rcoef[2 * RF + c]; }
   const auto dxr = make_rsrc(dx + off, pb);
   const auto drr = make_rsrc(RES ? dr + off : dx + off, RES ? pb : 0u);
 #pragma unroll
@@ -1277,39 +1235,12 @@ int sgcn_bn_eval_coef(int F, int perm_V, const float* gamma, const float* beta,
   return 0;
 }
 
-static int fold_check(const sgcn_bn_fold* f) {
-  SGCN_REQUIRE(!f || (f->part && f->n_part > 0 && f->mean && f->invstd && f->scale &&
-                      f->shift && (f->running_mean == nullptr) == (f->running_var == nullptr)));
-  return 0;
-}
-
-// the finalize of a fold as its own launch (consumers that do not fold)
-static int fold_resolve(const sgcn_bn_fold* f, int B, int C, void* stream) {
-  return sgcn_bn_finalize((const float*)f->part, B, C, f->n_part, 0, f->gamma, f->beta, f->eps,
-                          f->momentum, f->running_mean, f->running_var, f->num_batches,
-                          f->mean, f->invstd, f->scale, f->shift, stream);
-}
-
 int sgcn_bn_apply(const float* x, const float* scale, const float* shift, int per_joint,
                   const float* r, const float* rscale, const float* rshift, int relu,
                   float* y, float* y_stats, const float* gather_m, float* y_gathered, int B,
                   int C, int T, int V, void* stream) {
-  return sgcn_bn_apply_fold(x, scale, shift, per_joint, nullptr, r, rscale, rshift, nullptr,
-                            relu, y, y_stats, gather_m, y_gathered, B, C, T, V, stream);
-}
-
-int sgcn_bn_apply_fold(const float* x, const float* scale, const float* shift, int per_joint,
-                       const sgcn_bn_fold* fold, const float* r, const float* rscale,
-                       const float* rshift, const sgcn_bn_fold* rfold, int relu, float* y,
-                       float* y_stats, const float* gather_m, float* y_gathered, int B, int C,
-                       int T, int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
-  if (fold_check(fold) || fold_check(rfold)) return SGCN_EINVAL;
-  SGCN_REQUIRE(!fold || per_joint == 0);
-  SGCN_REQUIRE(!rfold || (r && !rscale && !rshift));
-  if (fold) { scale = fold->scale; shift = fold->shift; }
-  if (rfold) { rscale = rfold->scale; rshift = rfold->shift; }
   SGCN_REQUIRE(x && scale && shift && y);
   SGCN_REQUIRE((gather_m == nullptr) == (y_gathered == nullptr));
   SGCN_REQUIRE(!(y_stats && y_gathered) && y_gathered != y);
@@ -1325,10 +1256,9 @@ int sgcn_bn_apply_fold(const float* x, const float* scale, const float* shift, i
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
       const int ox = ys ? 1 : (y_gathered ? 2 : 0);
-      const sgcn_bn_fold fm = fold ? *fold : sgcn_bn_fold{}, fr = rfold ? *rfold : sgcn_bn_fold{};
 #define SGCN_AJ(NT, L, PJ, RS, RL, OX, ZU)                                                     \
   bn_apply_ja_kernel<NT, L, PJ, RS, RL, OX, ZU><<<g, NT, 0, st>>>(                             \
-      x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V, fm, fr)
+      x, scale, shift, r, rscale, rshift, y, ys, gather_m, y_gathered, C, T, V)
 #define SGCN_AJ_L(NT, PJ, RS, RL, OX, ZU)                                                      \
   do {                                                                                         \
     if (lpt == 8) SGCN_AJ(NT, 8, PJ, RS, RL, OX, ZU);                                          \
@@ -1374,9 +1304,6 @@ int sgcn_bn_apply_fold(const float* x, const float* scale, const float* shift, i
       return 0;
     }
   }
-  // the looping kernel reads finished coefficients: the folds' finalizes launch first
-  if (fold) { const int rc = fold_resolve(fold, B, C, stream); if (rc) return rc; }
-  if (rfold) { const int rc = fold_resolve(rfold, B, C, stream); if (rc) return rc; }
 #define SGCN_APPLY_X(PJ, RS, RL, OX)                                                        \
   bn_apply_kernel<PJ, RS, RL, OX><<<g, kThreads, 0, st>>>(x, scale, shift, r, rscale, rshift, y, \
                                                           ys, gather_m, y_gathered, C, T, V)
@@ -1491,37 +1418,12 @@ int sgcn_bn_bwd_finalize_gbn(const float* part6, int B, int C, int V, long long 
   return 0;
 }
 
-static int bwd_fold_check(const sgcn_bn_bwd_fold* f) {
-  SGCN_REQUIRE(!f || (f->part && f->mean && f->invstd && f->coef && f->n_total > 0));
-  return 0;
-}
-
-static int bwd_fold_resolve(const sgcn_bn_bwd_fold* f, int B, int C, void* stream) {
-  return sgcn_bn_bwd_finalize((const float*)f->part, B, C, (long long)f->n_total, 0, f->mean,
-                              f->invstd, f->gamma, f->dgamma, f->dbeta, 0, f->batch_stats,
-                              f->coef, stream);
-}
-
 int sgcn_bn_bwd_apply(const float* dy, const float* y, int relu, const float* x,
                       const float* coef, int per_joint, const float* r, const float* rcoef,
                       const float* dy_coef, float* dx, float* dr, int B, int C, int T, int V,
                       void* stream) {
-  return sgcn_bn_bwd_apply_fold(dy, y, relu, x, coef, per_joint, nullptr, r, rcoef, nullptr,
-                                dy_coef, dx, dr, B, C, T, V, stream);
-}
-
-int sgcn_bn_bwd_apply_fold(const float* dy, const float* y, int relu, const float* x,
-                           const float* coef, int per_joint, const sgcn_bn_bwd_fold* fold,
-                           const float* r, const float* rcoef, const sgcn_bn_bwd_fold* rfold,
-                           const float* dy_coef, float* dx, float* dr, int B, int C, int T,
-                           int V, void* stream) {
   SGCN_PLANE_CHECK();
   if (B == 0 || T == 0) return 0;
-  if (bwd_fold_check(fold) || bwd_fold_check(rfold)) return SGCN_EINVAL;
-  SGCN_REQUIRE(!fold || per_joint == 0);
-  SGCN_REQUIRE(!rfold || (r && dr && !rcoef));
-  if (fold) coef = fold->coef;
-  if (rfold) rcoef = rfold->coef;
   SGCN_REQUIRE(dy && x && coef && dx && (y || !relu));
   SGCN_REQUIRE(!dy_coef || (y && relu));
   SGCN_REQUIRE(!rcoef || (r && dr));
@@ -1535,13 +1437,11 @@ int sgcn_bn_bwd_apply_fold(const float* dy, const float* y, int relu, const floa
     const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
-      const sgcn_bn_bwd_fold fm = fold ? *fold : sgcn_bn_bwd_fold{};
-      const sgcn_bn_bwd_fold fr = rfold ? *rfold : sgcn_bn_bwd_fold{};
 #define SGCN_BJ(NT, L, PJ, RL, RS)                                                             \
   (dy_coef ? bn_bwd_apply_ja_kernel<NT, L, PJ, RL, RS, true><<<g, NT, 0, st>>>(                 \
-                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V, fm, fr)             \
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V)             \
            : bn_bwd_apply_ja_kernel<NT, L, PJ, RL, RS, false><<<g, NT, 0, st>>>(                \
-                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V, fm, fr))
+                 dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V))
 #define SGCN_BJ_L(NT, PJ, RL, RS)                                                              \
   do {                                                                                         \
     if (lpt == 8) SGCN_BJ(NT, 8, PJ, RL, RS);                                                  \
@@ -1568,8 +1468,6 @@ int sgcn_bn_bwd_apply_fold(const float* dy, const float* y, int relu, const floa
       return 0;
     }
   }
-  if (fold) { const int rc = bwd_fold_resolve(fold, B, C, stream); if (rc) return rc; }
-  if (rfold) { const int rc = bwd_fold_resolve(rfold, B, C, stream); if (rc) return rc; }
 #define SGCN_BA(PJ, RL, RS)                                                                   \
   (dy_coef ? bn_bwd_apply_kernel<PJ, RL, RS, true><<<g, kThreads, 0, st>>>(                      \
                  dy, y, x, coef, F, r, rcoef, C, dy_coef, dx, dr, C, T, V)                      \

@@ -171,8 +171,7 @@ __host__ __device__ inline Moments merge(Moments a, Moments b) {
 
 // Training-mode BatchNorm coefficients from the batch sums of per-plane {mean, M2}
 // partials (all B partials over n_part elements each): smean = sum mean_b, sm2 = sum M2_b,
-// smean2 = sum mean_b^2, in double. Shared by bn_finalize_kernel and the folded finalize
-// (bn_fold_channel), so both compute bit-identical values.
+// smean2 = sum mean_b^2, in double (bn_finalize_kernel).
 struct BnCoef {
   float mean, invstd, scale, shift;
   double unbiased;
@@ -197,76 +196,8 @@ __device__ __forceinline__ void bn_running_update(float* rm, float* rv, int rf, 
   rv[rf] = (1.f - momentum) * rv[rf] + momentum * (float)c.unbiased;
 }
 
-// The batch partials of channel c (part[b*C + c], b < B) as the three double sums of
-// bn_finalize_kernel's feature_sums, in ITS order — sample b into partial sum (b mod 8) in
-// increasing b, the eight merged 0..7 — so the folded coefficients are bit-identical to the
-// separate finalize's. One global round trip: every thread loads one partial into LDS, then
-// eight threads add theirs in order. NSUM = 2 (backward: sum g, sum g*xhat) or 3 (forward:
-// sum mean, sum M2, sum mean^2). Result in thread 0; call from all threads (2 barriers).
-constexpr int kFoldMaxB = 512;   // batch planes staged in LDS (more: direct loads)
-template <int NSUM>
-__device__ __forceinline__ void fold_sums(const float2* __restrict__ part, int c, int C, int B,
-                                          double (&out)[3]) {
-  __shared__ float2 pv_s[kFoldMaxB];
-  __shared__ double fs[8][3];
-  const int t = threadIdx.x, nt = blockDim.x;
-  const bool staged = B <= kFoldMaxB;
-  if (staged)
-    for (int b = t; b < B; b += nt) pv_s[b] = part[(size_t)b * C + c];
-  __syncthreads();
-  if (t < 8) {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-    for (int b = t; b < B; b += 8) {
-      const float2 pv = staged ? pv_s[b] : part[(size_t)b * C + c];
-      a0 += pv.x;
-      a1 += pv.y;
-      if (NSUM == 3) a2 += (double)pv.x * pv.x;
-    }
-    fs[t][0] = a0;
-    fs[t][1] = a1;
-    fs[t][2] = a2;
-  }
-  __syncthreads();
-  if (t == 0) {
-    out[0] = fs[0][0];
-    out[1] = fs[0][1];
-    out[2] = fs[0][2];
-    for (int q = 1; q < 8; ++q) {
-      out[0] += fs[q][0];
-      out[1] += fs[q][1];
-      out[2] += fs[q][2];
-    }
-  }
-}
-
-// The folded per-channel finalize (sgcn_bn_fold): returns channel c's (scale, shift) to
-// every thread of the workgroup (call from all threads: three barriers); the workgroup of
-// sample 0 also writes the statistics and the running-stat update.
-__device__ __forceinline__ float2 bn_fold_channel(const sgcn_bn_fold& f, int c, int C, int b,
-                                                  int B) {
-  __shared__ float2 fr;
-  double sm[3];
-  fold_sums<3>((const float2*)f.part, c, C, B, sm);
-  if (threadIdx.x == 0) {
-    const float g = f.gamma ? f.gamma[c] : 1.f;
-    const float be = f.beta ? f.beta[c] : 0.f;
-    const BnCoef k = bn_train_coef(sm[0], sm[1], sm[2], B, f.n_part, f.eps, g, be);
-    fr = make_float2(k.scale, k.shift);
-    if (b == 0) {
-      f.mean[c] = k.mean;
-      f.invstd[c] = k.invstd;
-      f.scale[c] = k.scale;
-      f.shift[c] = k.shift;
-      if (f.running_mean) bn_running_update(f.running_mean, f.running_var, c, f.momentum, k);
-      if (c == 0 && f.num_batches) *f.num_batches += 1;
-    }
-  }
-  __syncthreads();
-  return fr;
-}
-
 // Training BatchNorm backward coefficients (dx = k1*g + k2*x + k3) from the batch sums
-// sg = sum g, sgx = sum g*xhat (bn_bwd_finalize_kernel's math; shared with the fold).
+// sg = sum g, sgx = sum g*xhat (bn_bwd_finalize_kernel's math).
 __device__ __forceinline__ float3 bn_bwd_coef(double sg, double sgx, float g, float is,
                                               float mean, double n_total, int batch_stats) {
   const float k1 = g * is;
@@ -275,30 +206,6 @@ __device__ __forceinline__ float3 bn_bwd_coef(double sg, double sgx, float g, fl
   const float k3 = batch_stats ? (float)(-(double)k1 * (sg / n_total) - (double)k2 * (double)mean)
                                : 0.f;
   return make_float3(k1, k2, k3);
-}
-
-// The folded backward finalize (sgcn_bn_bwd_fold): channel c's (k1, k2, k3) to every
-// thread (call from all threads); sample 0's workgroup writes coef and dgamma/dbeta.
-__device__ __forceinline__ float3 bn_bwd_fold_channel(const sgcn_bn_bwd_fold& f, int c, int C,
-                                                      int b, int B) {
-  __shared__ float3 fr;
-  double sm[3];
-  fold_sums<2>((const float2*)f.part, c, C, B, sm);
-  if (threadIdx.x == 0) {
-    const float g = f.gamma ? f.gamma[c] : 1.f;
-    const float3 k = bn_bwd_coef(sm[0], sm[1], g, f.invstd[c], f.mean[c], f.n_total,
-                                 f.batch_stats);
-    fr = k;
-    if (b == 0) {
-      if (f.dgamma) f.dgamma[c] = (float)sm[1];
-      if (f.dbeta) f.dbeta[c] = (float)sm[0];
-      f.coef[c] = k.x;
-      f.coef[C + c] = k.y;
-      f.coef[2 * C + c] = k.z;
-    }
-  }
-  __syncthreads();
-  return fr;
 }
 
 }  // namespace sgcn

@@ -33,21 +33,21 @@ __global__ __launch_bounds__(kSgdThreads) void sgd_step_kernel(
   const int t = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
   const SgdEntry e = table[t];
   float* __restrict__ p = reinterpret_cast<float*>(e.p);
-  const float* __restrict__ g = reinterpret_cast<const float*>(e.g);
+  // the gradient is read and (scaled) written back through one pointer: no __restrict__
+  float* g = reinterpret_cast<float*>(e.g);
   float* __restrict__ buf = reinterpret_cast<float*>(e.buf);
   const float wd = __uint_as_float((unsigned)(e.wdlr & 0xffffffffLL));
   const float lr = __uint_as_float((unsigned)((unsigned long long)e.wdlr >> 32));
   const bool first = (e.flags & 1) != 0;
   const bool scaled = (e.flags & 2) != 0;
   const float gs = __uint_as_float((unsigned)((unsigned long long)e.flags >> 32));
-  float* __restrict__ gw = reinterpret_cast<float*>(e.g);
   const int end = min(numel[t], start + kSgdChunk);
   for (int i = start + (int)threadIdx.x; i < end; i += kSgdThreads) {
     const float pv = p[i];
     float d = g[i];
     if (scaled) {                                      // the reduction's grad *= 1/world
       d = d * gs;
-      gw[i] = d;
+      g[i] = d;
     }
     if (wd != 0.f) d = d + wd * pv;                    // grad + weight_decay * param
     float b;

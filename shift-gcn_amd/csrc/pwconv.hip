@@ -90,12 +90,6 @@ struct FwdArgs {
   // extent loads 0 / drops the store) and epilogue flags
   unsigned x_bytes, y_bytes, a_bytes, mask_bytes;
   int relu;
-  // EPI (inference Shift_gcn tail in the epilogue): per-(output row, stored joint) affine
-  // tables es/et [M][V] and the residual plane er (y's layout, er_bytes)
-  const float* es;
-  const float* et;
-  const float* er;
-  unsigned er_bytes;
 };
 
 // the FastDiv constants of a.T * a.V and a.V (every FwdArgs launch sets them)
@@ -105,15 +99,6 @@ inline void fwd_divisors(FwdArgs& a) {
   a.divN_s = n.s;
   a.divV_m = v.m;
   a.divV_s = v.s;
-}
-
-// relu(v * s + t + r) in this order, no contraction (the tshift_fwd_pre_kernel expression
-// of the same eval-mode Shift_gcn tail)
-__device__ __forceinline__ float epi_tail(float v, float s, float t, float r) {
-#pragma clang fp contract(off)
-  float h = v * s + t;
-  h += r;
-  return fmaxf(h, 0.f);
 }
 
 // Diagnostic builds only (tools/bench/pwbench -DSGCN_PW_STAMPS): per-workgroup cycle
@@ -251,11 +236,10 @@ __global__ void tshift_params_kernel(const float* __restrict__ xpos,
 // cost VALU per loaded element.
 // ------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM,
-          bool TSH = false, bool EPI = false>
+          bool TSH = false>
 __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   SGCN_CRIT_PRIO();
   static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
-  static_assert(!EPI || !ACCUM, "the eval tail epilogue stores");
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = 16;
   constexpr int MI = BM / WM / 32;
@@ -478,17 +462,12 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
     vq[q] = v_s[lane + 64 * q];
   }
   const bool rotated = p.y.rsign != 0;
-  const auto err = make_rsrc(EPI ? p.er : p.y.ptr, EPI ? p.er_bytes : 0u);
-  const unsigned tab_bytes = EPI ? (unsigned)(M * V * 4) : 0u;
-  const auto esr = make_rsrc(EPI ? p.es : p.y.ptr, tab_bytes);
-  const auto etr = make_rsrc(EPI ? p.et : p.y.ptr, tab_bytes);
   constexpr int RPW = RB / NW;     // rows per wave per pass
   static_assert(RB % NW == 0, "rows per wave");
-  // the global loads an output element needs besides the accumulator (EPI: its two
-  // BatchNorm coefficients and the residual; ACCUM: the old value) are issued for all of
-  // this wave's rows of a pass BEFORE the pass's LDS staging: in the store loop they would
-  // each wait a memory round trip (a load after the previous row's stores)
-  constexpr int NPF = EPI ? 3 : (ACCUM ? 1 : 0);
+  // the global load an output element needs besides the accumulator (ACCUM: the old
+  // value) is issued for all of this wave's rows of a pass BEFORE the pass's LDS staging: in
+  // the store loop it would wait a memory round trip (a load after the previous row's stores)
+  constexpr int NPF = ACCUM ? 1 : 0;
   float pf[NPF ? RPW : 1][NPF ? CQ : 1][NPF ? NPF : 1];
   auto row_of = [&](int i, int h, int k) {   // (tile row, its store row offset)
     const int lr = wid + k * NW;
@@ -518,18 +497,11 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
             const int trow = row_of(i, h, k);
             // a row past M: every address past its extent (loads 0, nothing stored later)
             const unsigned soff = m0 + trow < M ? (unsigned)(m0 + trow) * ycs4 : p.y_bytes;
-            const unsigned toff = m0 + trow < M ? (unsigned)((m0 + trow) * V) * 4u : tab_bytes;
 #pragma unroll
             for (int q = 0; q < CQ; ++q) {
               const int vo = voff_of(trow, q);
               const unsigned voff = ycolq[q] + (unsigned)(vo * 4);
-              if constexpr (EPI) {
-                pf[k][q][0] = bload(esr, (unsigned)vo * 4u, toff);
-                pf[k][q][1] = bload(etr, (unsigned)vo * 4u, toff);
-                pf[k][q][2] = bload(err, voff, soff);
-              } else if constexpr (ACCUM) {
-                pf[k][q][0] = bload(yr, voff, soff);
-              }
+              pf[k][q][0] = bload(yr, voff, soff);
             }
           }
         }
@@ -553,13 +525,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
           for (int q = 0; q < CQ; ++q) {
             const unsigned voff = ycolq[q] + (unsigned)(voff_of(trow, q) * 4);
             float val = smem[lr * BN + lane + 64 * q] + bv;
-            if constexpr (EPI) {
-              // BatchNorm1d(V*C) eval coefficients of the stored (channel, joint), the
-              // residual at the stored address, ReLU (shift_gcn.py:137-141)
-              val = epi_tail(val, pf[k][q][0], pf[k][q][1], pf[k][q][2]);
-            } else if (RELU) {
-              val = fmaxf(val, 0.f);
-            }
+            if (RELU) val = fmaxf(val, 0.f);
             if constexpr (ACCUM) val += pf[k][q][0];
             bstore(yr, val, voff, soff);
           }
@@ -1214,18 +1180,6 @@ void launch_pwg(const FwdArgs& a, bool accum, hipStream_t st) {
 }
 
 template <int BM, int BN, int WM, int WN>
-void launch_pwg_epi(const FwdArgs& a, hipStream_t st) {
-  const long long P = (long long)a.B * a.T * a.V;
-  dim3 grid((unsigned)((P + BN - 1) / BN), (a.M + BM - 1) / BM);
-  if (a.a_mcontig)
-    pwg_fwd_kernel<BM, BN, WM, WN, false, false, true, false, false, true>
-        <<<grid, 64 * WM * WN, 0, st>>>(a);
-  else
-    pwg_fwd_kernel<BM, BN, WM, WN, false, false, false, false, false, true>
-        <<<grid, 64 * WM * WN, 0, st>>>(a);
-}
-
-template <int BM, int BN, int WM, int WN>
 void launch_pwg_tsh(const FwdArgs& a, hipStream_t st) {
   const long long P = (long long)a.B * a.T * a.V;
   dim3 grid((unsigned)((P + BN - 1) / BN), (a.M + BM - 1) / BM);
@@ -1425,50 +1379,6 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   // tiles at M > 128 measured there too, not better)
   else if (M <= 128) launch_pwg<128, 128, 4, 2>(a, ac, st);
   else launch_pwg<256, 128, 4, 2>(a, ac, st);
-  SGCN_LAUNCH_CHECK();
-  return 0;
-}
-
-int sgcn_pw_fwd_bn_res(const float* w, int w_mcontig, const float* bias, const float* x,
-                       long long x_bstride, long long x_cstride, const float* out_scale,
-                       const float* out_shift, const float* res, float* y,
-                       long long y_bstride, long long y_cstride, int y_rsign, int B, int M,
-                       int K, int T, int V, void* stream) {
-  SGCN_REQUIRE(B >= 0 && M > 0 && K > 0 && K <= 256 && M <= 256 && T >= 0 && V > 0 &&
-               V < 32768);
-  SGCN_REQUIRE(y_rsign >= -1 && y_rsign <= 1);
-  SGCN_REQUIRE(x_cstride >= (long long)T * V && y_cstride >= (long long)T * V);
-  SGCN_REQUIRE(x_cstride * (long long)K < (1LL << 31) && y_cstride * (long long)M < (1LL << 31));
-  SGCN_REQUIRE((long long)B * T * V < (1LL << 31));
-  SGCN_REQUIRE((long long)(B - 1) * x_bstride + (long long)K * x_cstride + (long long)T * V < (1LL << 29));
-  SGCN_REQUIRE((long long)(B - 1) * y_bstride + (long long)M * y_cstride + (long long)T * V < (1LL << 29));
-  if (B == 0 || T == 0) return 0;
-  SGCN_REQUIRE(w && x && y && out_scale && out_shift && res);
-  FwdArgs a{};
-  a.A = w;
-  a.lda = w_mcontig ? M : K;
-  a.a_mcontig = w_mcontig;
-  a.bias = bias;
-  a.x = {x, x_bstride, x_cstride, 1, 0};
-  a.y = {y, y_bstride, y_cstride, 1, y_rsign};
-  a.M = M;
-  a.K = K;
-  a.T = T;
-  a.V = V;
-  a.B = B;
-  fwd_divisors(a);
-  a.x_bytes = plane_bytes(x_bstride, x_cstride, 1, B, K, T, V);
-  a.y_bytes = plane_bytes(y_bstride, y_cstride, 1, B, M, T, V);
-  a.a_bytes = (unsigned)((long long)M * K * 4);
-  a.relu = 1;
-  a.es = out_scale;
-  a.et = out_shift;
-  a.er = res;
-  a.er_bytes = a.y_bytes;   // the residual has y's layout
-  hipStream_t st = (hipStream_t)stream;
-  if (M <= 64) launch_pwg_epi<64, 256, 2, 4>(a, st);
-  else if (M <= 128) launch_pwg_epi<128, 256, 2, 4>(a, st);
-  else launch_pwg_epi<256, 128, 4, 2>(a, st);
   SGCN_LAUNCH_CHECK();
   return 0;
 }

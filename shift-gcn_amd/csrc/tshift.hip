@@ -460,8 +460,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     int Ho, int stride, int add_half, const float* __restrict__ zs = nullptr,
     const float* __restrict__ zt = nullptr, const float* __restrict__ r = nullptr,
     const float* __restrict__ rs = nullptr, const float* __restrict__ rt = nullptr,
-    const float* __restrict__ gm = nullptr, float* __restrict__ og = nullptr,
-    const sgcn_bn_fold fa = sgcn_bn_fold{}) {
+    const float* __restrict__ gm = nullptr, float* __restrict__ og = nullptr) {
   SGCN_CRIT_PRIO();
   static_assert(MODE != 1 || (AFFINE && RES >= 1 && !STATS), "pre: affine taps of relu(...)");
   static_assert(MODE != 2 || (!AFFINE && !STATS), "tail: plain taps");
@@ -476,8 +475,7 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
   const int nb = Hb * W, n = Ho * W;
   const unsigned vo = own ? (unsigned)tid * 4u : 0x80000000u, vstep = (unsigned)NTJ * 4u;
   float a = 1.f, b = 0.f;
-  const bool fold = MODE == 0 && AFFINE && fa.part != nullptr;   // uniform
-  if (AFFINE && !fold) { a = scale[c]; b = shift[c]; }
+  if (AFFINE) { a = scale[c]; b = shift[c]; }
   float q1 = 1.f, q2 = 0.f;   // residual BatchNorm (RES 2)
   if (RES == 2) { q1 = rs[c]; q2 = rt[c]; }
   {
@@ -485,11 +483,6 @@ __global__ __launch_bounds__(NT) void tshift_fwd_pad_kernel(
     float t[LPT], u[MODE == 1 ? LPT : 1];
 #pragma unroll
     for (int e = 0; e < LPT; ++e) t[e] = bload(ir, vo + e * vstep, 0);
-    if (fold) {   // the BatchNorm finalize of the input, while the plane's loads fly
-      const float2 ab = bn_fold_channel(fa, c, C, plane / C, (int)gridDim.x / C);
-      a = ab.x;
-      b = ab.y;
-    }
     if (MODE == 1) {
       const auto rr = make_rsrc(r + (size_t)plane * nb, (unsigned)nb * 4u);
 #pragma unroll
@@ -949,7 +942,7 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
     const float* __restrict__ gz, const float* __restrict__ gzm,
     const float* __restrict__ gzi, float* __restrict__ gzpart, const float* __restrict__ gd = nullptr,
     const float* __restrict__ gdm = nullptr, const float* __restrict__ gdi = nullptr,
-    float* __restrict__ gdpart = nullptr, const sgcn_bn_bwd_fold gf = sgcn_bn_bwd_fold{}) {
+    float* __restrict__ gdpart = nullptr) {
   SGCN_CRIT_PRIO();
   static_assert(!GBN || (AFFINE && BNP && !GP), "GBN: shift_in with BNP");
   static_assert(!GBD || GBN, "GBD extends GBN");
@@ -991,19 +984,8 @@ __global__ __launch_bounds__(NT) void tshift_bwd_ra_kernel(
         u2[e] = bload(xr, vb, 0);
         rin_r[e] = bload(inr, vb, 0);
       }
-      // bn2's backward coefficients: read, or its backward finalize folded in (uniform),
-      // while the plane's loads fly
-      float k1, k2, k3;
-      if (gf.part) {
-        const float3 k = bn_bwd_fold_channel(gf, c, C, plane / C, (int)gridDim.x / C);
-        k1 = k.x;
-        k2 = k.y;
-        k3 = k.z;
-      } else {
-        k1 = gcoef[c];
-        k2 = gcoef[C + c];
-        k3 = gcoef[2 * C + c];
-      }
+      // bn2's backward coefficients, read while the plane's loads fly
+      const float k1 = gcoef[c], k2 = gcoef[C + c], k3 = gcoef[2 * C + c];
 #pragma unroll
       for (int e = 0; e < LPT; ++e) t[e] = k1 * (u1[e] > 0.f ? t[e] : 0.f) + k2 * u2[e] + k3;
     } else {
@@ -1339,15 +1321,14 @@ template <int NT>
 bool launch_fwd_pad(bool affine, bool stats, const float* in, float* out, const float* xpos,
                     const float* ypos, const float* scale, const float* shift, float2* ps,
                     int B, int C, int H, int W, int Ho, int stride, int add_half,
-                    hipStream_t st, const sgcn_bn_fold* fold = nullptr) {
+                    hipStream_t st) {
   const int lpt = pad_fwd_lpt(H, W, NT);
   const size_t lds = (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float);
   if (lpt == 0) return false;
-  const sgcn_bn_fold fa = fold ? *fold : sgcn_bn_fold{};
 #define SGCN_FWDP(L, A, S)                                                                   \
   tshift_fwd_pad_kernel<NT, L, 0, A, S><<<B * C, NT, lds, st>>>(                             \
       in, out, xpos, ypos, scale, shift, ps, C, H, W, Ho, stride, add_half, nullptr, nullptr, \
-      nullptr, nullptr, nullptr, nullptr, nullptr, fa)
+      nullptr, nullptr, nullptr, nullptr, nullptr)
 #define SGCN_FWDP_AS(L)                                                                      \
   do {                                                                                       \
     if (affine) { if (stats) SGCN_FWDP(L, true, true); else SGCN_FWDP(L, true, false); }     \
@@ -1450,16 +1431,14 @@ bool launch_ra(int nt, const float* gout, const float* in, const float* xpos,
                int W, const float* gdy, const float* gy, const float* gx, const float* gcoef,
                const float* gz, const float* gzm, const float* gzi, float* gzpart,
                hipStream_t st, const float* gd = nullptr, const float* gdm = nullptr,
-               const float* gdi = nullptr, float* gdpart = nullptr,
-               const sgcn_bn_bwd_fold* gfold = nullptr) {
+               const float* gdi = nullptr, float* gdpart = nullptr) {
   const int lpt = ra_lpt(H * W, nt, W);
   const size_t lds = ra_lds_bytes(H, W, nt, GBN);
   if (lpt == 0 || lds > kRaLdsMax) return false;
-  const sgcn_bn_bwd_fold gf = gfold ? *gfold : sgcn_bn_bwd_fold{};
 #define SGCN_RA(NT, L)                                                                         \
   tshift_bwd_ra_kernel<NT, L, AFFINE, RELU, BNP, GP, GBN, GBD><<<B * C, NT, lds, st>>>(        \
       gout, in, xpos, ypos, scale, shift, bmu, bis, gin, pg, bp, C, H, W, gdy, gy, gx, gcoef,  \
-      gz, gzm, gzi, gzpart, gd, gdm, gdi, gdpart, gf)
+      gz, gzm, gzi, gzpart, gd, gdm, gdi, gdpart)
   if (nt == 256) {
     if (lpt == 8) SGCN_RA(256, 8); else if (lpt == 16) SGCN_RA(256, 16); else if (lpt == 24) SGCN_RA(256, 24); else SGCN_RA(256, 32);
   } else {
@@ -1523,40 +1502,6 @@ int sgcn_tshift_fwd(const float* in, float* out, const float* xpos, const float*
   }
   SGCN_LAUNCH_CHECK();
   return 0;
-}
-
-int sgcn_tshift_fwd_fold(const float* in, float* out, const float* xpos, const float* ypos,
-                         const sgcn_bn_fold* fold, float* plane_stats, int B, int C, int H,
-                         int W, int stride, int ypos_is_raw, void* stream) {
-  if (!fold)
-    return sgcn_tshift_fwd(in, out, xpos, ypos, nullptr, nullptr, plane_stats, B, C, H, W,
-                           stride, ypos_is_raw, stream);
-  SGCN_REQUIRE(B >= 0 && C > 0 && H >= 0 && W > 0 && stride >= 1);
-  SGCN_REQUIRE(fold->part && fold->n_part > 0 && fold->mean && fold->invstd && fold->scale &&
-               fold->shift && (fold->running_mean == nullptr) == (fold->running_var == nullptr));
-  const int Ho = H / stride;
-  if (B == 0 || Ho == 0) return 0;
-  SGCN_REQUIRE(in && out && xpos && ypos);
-  SGCN_REQUIRE((long long)H * W < (1LL << 30) && (long long)B * C < (1LL << 31));
-  hipStream_t st = (hipStream_t)stream;
-  const bool stats = plane_stats != nullptr;
-  float2* ps = (float2*)plane_stats;
-  const int ah = (ypos_is_raw && stride != 1) ? 1 : 0;
-  if (H * W <= kFwdLdsMax2 &&
-      (H * W <= kFwdLdsMax
-           ? launch_fwd_pad<kThreads>(true, stats, in, out, xpos, ypos, fold->scale, fold->shift, ps, B, C, H, W, Ho, stride, ah, st, fold)
-           : launch_fwd_pad<512>(true, stats, in, out, xpos, ypos, fold->scale, fold->shift, ps, B, C, H, W, Ho, stride, ah, st, fold))) {
-    SGCN_LAUNCH_CHECK();
-    return 0;
-  }
-  // planes the padded kernel does not take: the finalize as its own launch
-  const int rc = sgcn_bn_finalize((const float*)fold->part, B, C, fold->n_part, 0, fold->gamma,
-                                  fold->beta, fold->eps, fold->momentum, fold->running_mean,
-                                  fold->running_var, fold->num_batches, fold->mean,
-                                  fold->invstd, fold->scale, fold->shift, stream);
-  if (rc) return rc;
-  return sgcn_tshift_fwd(in, out, xpos, ypos, fold->scale, fold->shift, plane_stats, B, C, H,
-                         W, stride, ypos_is_raw, stream);
 }
 
 int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const float* ypos,
@@ -1692,20 +1637,8 @@ int sgcn_tshift_bwd_bnin(const float* dy, const float* y, const float* s, const 
                          const float* in, const float* xpos, const float* ypos, float* gin,
                          float* gx, float* gy, void* ws, size_t ws_bytes, int B, int C, int H,
                          int W, int ypos_is_raw, void* stream) {
-  return sgcn_tshift_bwd_bnin_fold(dy, y, s, coef, nullptr, in, xpos, ypos, gin, gx, gy, ws,
-                                   ws_bytes, B, C, H, W, ypos_is_raw, stream);
-}
-
-int sgcn_tshift_bwd_bnin_fold(const float* dy, const float* y, const float* s,
-                              const float* coef, const sgcn_bn_bwd_fold* fold, const float* in,
-                              const float* xpos, const float* ypos, float* gin, float* gx,
-                              float* gy, void* ws, size_t ws_bytes, int B, int C, int H, int W,
-                              int ypos_is_raw, void* stream) {
   SGCN_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0);
   SGCN_REQUIRE(H * W <= kBwdLdsMax);   // LDS-staged stride-1 planes only (caller falls back)
-  SGCN_REQUIRE(!fold || (fold->part && fold->mean && fold->invstd && fold->coef &&
-                         fold->n_total > 0));
-  if (fold) coef = fold->coef;
   SGCN_REQUIRE(dy && y && s && coef && in && xpos && ypos && gin && ws);
   SGCN_REQUIRE((gx == nullptr) == (gy == nullptr));
   SGCN_REQUIRE(ws_bytes >= sgcn_tshift_bwd_ws_bytes(B, C));
@@ -1718,8 +1651,7 @@ int sgcn_tshift_bwd_bnin_fold(const float* dy, const float* y, const float* s,
   const int ntb = H * W <= 4096 ? 256 : 512;
   const bool ok = launch_ra<false, true, false, true, false>(
       ntb, nullptr, in, xpos, ypos, nullptr, nullptr, nullptr, nullptr, gin, pg, nullptr, B, C,
-      H, W, dy, y, s, coef, nullptr, nullptr, nullptr, nullptr, st, nullptr, nullptr, nullptr,
-      nullptr, fold);
+      H, W, dy, y, s, coef, nullptr, nullptr, nullptr, nullptr, st);
   SGCN_REQUIRE(ok);   // W <= 64, <= 32 elements per thread, padded plane <= 64 KiB (ops.ra_fits)
   SGCN_LAUNCH_CHECK();
   if (gx) tshift_pos_finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(pg, B, C, gx, gy);

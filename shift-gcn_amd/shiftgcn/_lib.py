@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # same-box A/B of two builds (tuning only, e.g. tools/ab_lib.sh): another in-tree build of
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
-ABI_VERSION = 21
+ABI_VERSION = 22
 BATCH_MAX = 32            # include/shiftgcn.h SGCN_BATCH_MAX
 ABI_DIAG_FLAG = 0x10000   # include/shiftgcn.h SGCN_ABI_DIAG_FLAG: a diagnostic build
 EINVAL = -22
@@ -50,8 +50,6 @@ SIGNATURES = {
                                  _P]),
     "sgcn_pw_fwd": (_I, [_P, _I, _P, _P, _L, _L, _I, _I, _P, _P, _L, _L, _I, _I, _I, _I, _I,
                          _I, _I, _I, _I, _P]),
-    "sgcn_pw_fwd_bn_res": (_I, [_P, _I, _P, _P, _L, _L, _P, _P, _P, _P, _L, _L, _I, _I, _I, _I,
-                                _I, _I, _P]),
     "sgcn_pw_tshift_ws_bytes": (_Z, [_I]),
     "sgcn_pw_fwd_tshift": (_I, [_P, _P, _P, _L, _L, _P, _P, _P, _P, _P, _P, _Z, _P, _L, _L, _I,
                                 _I, _I, _I, _I, _I, _P]),
@@ -65,13 +63,6 @@ SIGNATURES = {
     "sgcn_bn_eval_coef": (_I, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P]),
     "sgcn_bn_apply": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I,
                            _P]),
-    "sgcn_bn_apply_fold": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I,
-                                _I, _I, _P]),
-    "sgcn_tshift_fwd_fold": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
-    "sgcn_tshift_bwd_bnin_fold": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I,
-                                       _I, _I, _I, _I, _P]),
-    "sgcn_bn_bwd_apply_fold": (_I, [_P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I,
-                                    _I, _I, _P]),
     "sgcn_bn_bwd_reduce": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I,
                                 _I, _P]),
     "sgcn_bn_bwd_finalize": (_I, [_P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
@@ -99,10 +90,6 @@ SIGNATURES = {
     "sgcn_tshift_pos_finalize_many": (_I, [_P, _P, _P, _P, _P, _I, _P]),
     "sgcn_mask_prep_many": (_I, [_P, _P, _P, _I, _P]),
     "sgcn_mask_grad_finalize_many": (_I, [_P, _P, _P, _P, _P, _P, _I, _P]),
-    "sgcn_device_cu_count": (_I, [_I, _P]),
-    "sgcn_stream_create_cu_mask": (_I, [_P, _I, _P]),
-    "sgcn_stream_get_cu_mask": (_I, [_P, _P, _I]),
-    "sgcn_stream_destroy": (_I, [_P]),
 }
 
 

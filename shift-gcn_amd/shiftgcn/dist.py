@@ -86,7 +86,9 @@ class GradAllReduce:
     applied here (one multiply), or, with ``defer_scale_to`` = a :class:`FusedSGD`, inside
     that optimizer's update launch (flags bit 1 of ``sgcn_sgd_step``), which also stores the
     scaled gradient back, so ``.grad`` ends the step holding the same values either way. In
-    the deferred form ``.grad`` holds the rank SUM between this call and ``step()``."""
+    the deferred form ``.grad`` holds the rank SUM between this call and ``step()``: read or
+    clip gradients there only through :meth:`clip_grad_norm_` (or use the immediate form),
+    never with a plain ``clip_grad_norm_`` over ``.grad``."""
 
     def __init__(self, model: torch.nn.Module, group=None, shift_grad_rule: str = "sum",
                  defer_scale_to=None):
@@ -109,6 +111,7 @@ class GradAllReduce:
         self.copied = 0   # gradients copied into the bucket by the last call (diagnostics)
 
     def __call__(self):
+        from . import ops
         base = self.flat.data_ptr()
         copied = 0
         for (_, p), off, k in zip(self.named, self.offsets, self.sizes):
@@ -123,12 +126,25 @@ class GradAllReduce:
                 copied += 1
             p.grad = slot
         self.copied = copied
+        # the slots may be handed out again by the next backward (ops.grad_like)
+        ops.release_grad_slots([p for _, p in self.named])
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         if self.defer_to is not None:
             self.defer_to.defer_grad_scale(
                 [(p, s) for (_, p), s in zip(self.named, self.param_scale) if s != 1.0])
         else:
             self.flat.mul_(self.scale)
+
+    def clip_grad_norm_(self, max_norm: float, eps: float = 1e-6):
+        """``torch.nn.utils.clip_grad_norm_`` (2-norm) of the REDUCED gradients, right after
+        this call and before ``step()``, in both scale forms: with ``defer_scale_to`` the
+        bucket still holds the rank SUM, so the norm is taken of sum x scale and the clip
+        coefficient multiplies the bucket (the deferred scale follows in the update).
+        Returns the total norm (a device tensor)."""
+        g = self.flat * self.scale if self.defer_to is not None else self.flat
+        total = torch.linalg.vector_norm(g)
+        self.flat.mul_(torch.clamp(max_norm / (total + eps), max=1.0))
+        return total
 
     def close(self):
         """Unregister the bucket slots (the model's gradients go to fresh memory again)."""
@@ -139,10 +155,16 @@ class GradAllReduce:
 def broadcast_buffers(model: torch.nn.Module, src: int = 0, group=None):
     """Make every rank hold rank ``src``'s BatchNorm running statistics (DataParallel keeps
     replica 0's)."""
-    for b in model.buffers():
+    from .ops import bump_versions
+    bufs = list(model.buffers())
+    for b in bufs:
         dist.broadcast(b, src, group=group)
+    bump_versions(bufs)   # (eval-mode caches keyed on the running statistics' versions)
 
 
 def broadcast_parameters(model: torch.nn.Module, src: int = 0, group=None):
-    for p in model.parameters():
+    from .ops import bump_versions
+    ps = list(model.parameters())
+    for p in ps:
         dist.broadcast(p.data, src, group=group)
+    bump_versions(ps)

@@ -119,6 +119,16 @@ class Ensemble(nn.Module):
                              persistent=False)
 
     def _data_bn_coef(self):
+        """The four models' eval-mode data_bn coefficients, (4, F) each; computed once per
+        version of those BatchNorms (ops.cached)."""
+        bns = [m.data_bn for m in self.models]
+        key = ops._src_key([t for bn in bns for t in (bn.weight, bn.bias, bn.running_mean,
+                                                      bn.running_var)])
+        key += tuple(float(bn.eps) for bn in bns)
+        return ops.cached(self, "_sgcn_data_bn", key, self._make_data_bn_coef,
+                          self.parent.device)
+
+    def _make_data_bn_coef(self):
         F = self.models[0].data_bn.num_features
         dev = self.parent.device
         scale = torch.empty(4, F, device=dev, dtype=torch.float32)
@@ -167,14 +177,32 @@ class Ensemble(nn.Module):
         return scores, acc
 
 
+def _state_key(module):
+    """Storage and version of every parameter and buffer of ``module``."""
+    return ops._src_key(list(module.parameters()) + list(module.buffers()))
+
+
 class EnsembleGraph:
     """One hipGraph for a fixed batch shape: ``run(joint)`` copies the batch into the
     static input, replays the captured ensemble forward and returns (scores, logits)
-    (views of static outputs, overwritten by the next ``run``)."""
+    (views of static outputs, overwritten by the next ``run``).
+
+    The eval-mode constants (BatchNorm coefficients, masks, folded conv+BatchNorm weights)
+    are computed once per weight version outside the graph (ops.cached), so the graph holds
+    the contraction and streaming kernels only; if any parameter or buffer of the ensemble
+    has changed since the capture (an optimizer step, load_state_dict, a running-statistics
+    update), ``run`` captures again first."""
 
     def __init__(self, ensemble: Ensemble, batch_shape, device):
         self.ensemble = ensemble
+        self.device = device
         self.static_in = torch.zeros(batch_shape, device=device, dtype=torch.float32)
+        self.captures = 0
+        self._capture()
+
+    def _capture(self):
+        ensemble, device = self.ensemble, self.device
+        self.graph = None
         side = torch.cuda.Stream(device)
         side.wait_stream(torch.cuda.current_stream(device))
         with torch.cuda.stream(side):
@@ -184,8 +212,12 @@ class EnsembleGraph:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.scores, self.logits = ensemble(self.static_in)
+        self.key = _state_key(ensemble)
+        self.captures += 1
 
     def run(self, joint):
+        if _state_key(self.ensemble) != self.key:
+            self._capture()
         self.static_in.copy_(joint, non_blocking=True)
         self.graph.replay()
         return self.scores, self.logits

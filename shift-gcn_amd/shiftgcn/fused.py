@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import os
 import threading
+import weakref
 
 import torch
 
@@ -51,62 +52,12 @@ def _empty(*shape, like):
 # current stream before returning, so everything after loss.backward() sees finished grads.
 # --------------------------------------------------------------------------------------
 _SIDE = {}
-_MASKED = []   # keeps the CU-masked HIP streams alive for the process
-
-
-def cu_mask_bits(total, n, pattern):
-    """CU indices of an n-CU subset of ``total``: "low" = 0..n-1, "high" = the last n,
-    "spread" = every (total/n)-th."""
-    n = max(1, min(n, total))
-    if pattern == "high":
-        return list(range(total - n, total))
-    if pattern == "spread":
-        step = total / n
-        return sorted({int(i * step) for i in range(n)})
-    return list(range(n))
-
-
-def masked_stream(device, cus):
-    """A torch stream over a HIP stream restricted to the CU indices ``cus``
-    (sgcn_stream_create_cu_mask)."""
-    import ctypes
-
-    from . import _lib
-    lib = _lib.load()
-    dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    total = ctypes.c_int(0)
-    _lib.check(lib.sgcn_device_cu_count(idx, ctypes.byref(total)), "sgcn_device_cu_count")
-    words = (total.value + 31) // 32
-    mask = (ctypes.c_uint * words)()
-    for c in cus:
-        if 0 <= c < total.value:
-            mask[c // 32] |= 1 << (c % 32)
-    ptr = ctypes.c_void_p()
-    with torch.cuda.device(idx):
-        _lib.check(lib.sgcn_stream_create_cu_mask(mask, words, ctypes.byref(ptr)),
-                   "sgcn_stream_create_cu_mask")
-    st = torch.cuda.ExternalStream(ptr.value, device=dev)
-    _MASKED.append(st)
-    return st
 
 
 def _side_stream(device):
     s = _SIDE.get(device)
     if s is None:
-        if SIDE_CUS > 0:   # the side stream confined to SIDE_CUS CUs (A/B knob)
-            import ctypes
-
-            from . import _lib
-            total = ctypes.c_int(0)
-            dev = torch.device(device)
-            _lib.check(_lib.load().sgcn_device_cu_count(
-                dev.index if dev.index is not None else torch.cuda.current_device(),
-                ctypes.byref(total)), "sgcn_device_cu_count")
-            s = masked_stream(device, cu_mask_bits(total.value, SIDE_CUS, SIDE_CU_PATTERN))
-        else:
-            s = torch.cuda.Stream(device=device)
-        _SIDE[device] = s
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
     return s
 
 
@@ -237,7 +188,25 @@ def join_side(device):
 # Shift_gcn
 # ======================================================================================
 class GcnSaved:
-    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
+    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments", "shared",
+                 "__weakref__")
+
+
+def _register(mod, s):
+    """Record the forward state ``s`` of block ``mod`` among the block's live ones (weak:
+    one per graph that may yet run its backward). The deferred gradient writes (side stream,
+    end-of-backward finalizes) rely on autograd TAKING each returned gradient tensor as
+    ``.grad``; if the block's parameters get a second contribution in the same backward (the
+    block run twice in one graph), autograd sums the two tensors first — possibly before a
+    deferred launch has written one of them. So every state that was alive together with
+    another state of the same block is marked ``shared``, and its backward defers nothing."""
+    ws = mod.__dict__.get("_sgcn_live")
+    if ws is None:
+        ws = mod.__dict__["_sgcn_live"] = weakref.WeakSet()
+    s.shared = len(ws) > 0
+    for o in ws:
+        o.shared = True
+    ws.add(s)
 
 
 def gcn_forward(mod, x0, training, off=False):
@@ -252,8 +221,8 @@ def gcn_forward(mod, x0, training, off=False):
         down = _OffPath(off, x0)
         with down:
             ops.pw_fwd(conv.weight, False, conv.bias, PV(x0), PV(D0), Cout, Cin, T, V)
-            if training:   # (folded into the gcn tail's apply below)
-                dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn, defer=True)
+            if training:
+                dst = ops.bn_finalize(ops.moments(D0, False), B, Cout, T * V, bn)
             else:
                 dst = ops.bn_eval_coef(bn, Cout)
     cache = mod.__dict__.pop("_gather_cache", None)
@@ -278,21 +247,32 @@ def gcn_forward(mod, x0, training, off=False):
     s = GcnSaved()
     s.x0, s.xg, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, xg, Z, zst, D0, dst, H, m
     s.h_moments = hm   # moments of H for Shift_tcn.bn, produced by the same launch
+    _register(mod, s)
     return H, s
 
 
 def _mask_of(gcn):
     """tanh(Feature_Mask) + 1 of a Shift_gcn: the one linked_units prepared for this call
-    (all units' in one launch), else its own launch."""
+    (all units' in one launch), else its own launch (once per version of the mask)."""
+    fm = gcn.Feature_Mask
     r = gcn.__dict__.get("_mask_ready")
-    if r is not None and r[0] is gcn.Feature_Mask and r[1] == gcn.Feature_Mask._version:
+    if r is not None and r[0] is fm and r[1] == fm._version:
         return r[2]
-    return ops.mask_prep(gcn.Feature_Mask)
+    if gcn.training:
+        return ops.mask_prep(fm)
+    return ops.cached(gcn, "_sgcn_mask", ops._src_key((fm,)), lambda: ops.mask_prep(fm),
+                      fm.device)
 
 
 def prepare_masks(gcns):
-    """Every Shift_gcn's mask for one forward in one launch (sgcn_mask_prep_many)."""
-    ms = ops.mask_prep_many([g.Feature_Mask for g in gcns])
+    """Every Shift_gcn's mask for one forward in one launch (sgcn_mask_prep_many); in eval
+    mode once per version of the masks (ops.cached)."""
+    fms = [g.Feature_Mask for g in gcns]
+    if any(g.training for g in gcns):
+        ms = ops.mask_prep_many(fms)
+    else:
+        ms = ops.cached(gcns[0], "_sgcn_masks", ops._src_key(fms) + tuple(map(id, gcns)),
+                        lambda: ops.mask_prep_many(fms), fms[0].device)
     for g, m in zip(gcns, ms):
         g.__dict__["_mask_ready"] = (g.Feature_Mask, g.Feature_Mask._version, m)
 
@@ -358,10 +338,12 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     else:
         dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
     dmask = ops.grad_like(mod.Feature_Mask)
-    # (deferred only when autograd will TAKE dmask as .grad: an existing .grad would be
-    # accumulated into from dmask before the deferred launch writes it)
+    # (deferred only when autograd will TAKE dmask as .grad: an existing .grad, or a second
+    # contribution from another use of this block in the same graph, would be added to dmask
+    # before the deferred launch writes it)
     fm = mod.Feature_Mask
-    if (BATCH_SIDE and fm.grad is None and not getattr(fm, "_backward_hooks", None) and
+    if (BATCH_SIDE and fm.grad is None and not s.shared and
+            not getattr(fm, "_backward_hooks", None) and
             not getattr(fm, "_post_accumulate_grad_hooks", None) and
             (off or _flush_queued(mpart.device))):
         # with the backward's other optimizer-only finalizes (join_side / end of backward)
@@ -402,43 +384,17 @@ def folded_conv_bn(conv, bn):
     on the conv, keyed by the storage and version counters of every tensor it reads, so an
     optimizer step, load_state_dict or a device move recomputes it."""
     srcs = (conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var)
-    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in srcs)
-    key += (float(bn.eps),)
-    c = conv.__dict__.get("_sgcn_fold")
-    if c is not None and c[0] == key:
-        return c[1], c[2]
-    st = ops.bn_eval_coef(bn, conv.out_channels)
-    with torch.no_grad():
-        w = (conv.weight.detach() *
-             st.scale.view(-1, *([1] * (conv.weight.dim() - 1)))).contiguous()
-        b = (conv.bias.detach() * st.scale + st.shift if conv.bias is not None
-             else st.shift.clone())
-    conv.__dict__["_sgcn_fold"] = (key, w, b)
-    return w, b
+    key = ops._src_key(srcs) + (float(bn.eps),)
 
-
-def gcn_infer_h(mod, x0):
-    """Inference Shift_gcn in one contraction launch (sgcn_pw_fwd_bn_res): einsum +
-    Linear_bias, shift_out in the store addresses, BatchNorm1d(V*C) eval, + down (its
-    BatchNorm folded into the conv) or identity, ReLU, all in the epilogue; returns H."""
-    B, Cin, T, V = x0.shape
-    Cout = mod.out_channels
-    cache = mod.__dict__.pop("_gather_cache", None)
-    if cache is not None and cache[0] is x0:
-        xg = cache[1]
-    else:
-        xg = ops.gcn_gather(x0, _mask_of(mod))
-    if mod.has_down:
-        w, b = folded_conv_bn(mod.down[0], mod.down[1])
-        res = _empty(B, Cout, T, V, like=x0)
-        ops.pw_fwd(w, False, b, PV(x0), PV(res), Cout, Cin, T, V)
-    else:
-        res = x0
-    zst = ops.bn_eval_coef(mod.bn, Cout * V, perm_V=V)
-    H = _empty(B, Cout, T, V, like=x0)
-    ops.pw_fwd_bn_res(mod.Linear_weight, True, mod.Linear_bias, PV(xg), zst, res, PV(H, 1, +1),
-                      Cout, Cin, T, V)
-    return H
+    def make():
+        st = ops.bn_eval_coef(bn, conv.out_channels)
+        with torch.no_grad():
+            w = (conv.weight.detach() *
+                 st.scale.view(-1, *([1] * (conv.weight.dim() - 1)))).contiguous()
+            b = (conv.bias.detach() * st.scale + st.shift if conv.bias is not None
+                 else st.shift.clone())
+        return w, b
+    return ops.cached(conv, "_sgcn_fold", key, make, conv.weight.device)
 
 
 def convbn_infer_folded(mod, x):
@@ -491,8 +447,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
     if training:
         if h_moments is None:
             h_moments = ops.moments(H, False)
-        # folded into the shift_in launch (sgcn_tshift_fwd_fold)
-        ast = ops.bn_finalize(h_moments, B, C, T * V, mod.bn, defer=True)
+        ast = ops.bn_finalize(h_moments, B, C, T * V, mod.bn)
     else:
         ast = ops.bn_eval_coef(mod.bn, C)
     R = _empty(B, Cout, T, V, like=src)
@@ -502,11 +457,6 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
         As = ops.tshift_fwd_pre(pre[0], si.xpos.detach(), si.ypos.detach(), si.stride, pre[1],
                                 pre[2], pre[3], ast)
         ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
-    elif tail is not None and C >= EVAL_TSHIFT_FUSION_MIN_C:
-        # inference: shift_in (with bn's eval affine) formed in temporal_linear's operand
-        # staging; the shifted operand is neither stored nor read back
-        ops.pw_fwd_tshift(tl.weight, tl.bias, PV(H), si.xpos.detach(), si.ypos.detach(), ast,
-                          PV(R), Cout, C, T, V, relu=True)
     elif tshift_fused(C) and tail is None:
         # shift_in (with Shift_tcn.bn's apply) formed in the contraction's operand staging,
         # never read back; also stored from the same registers for the weight gradient
@@ -524,8 +474,8 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
                                    r=tail[0], rst=tail[1], gather_m=tail[2])
     stats = _empty(B * Cout * 2, like=src) if training else None
     S = ops.tshift_fwd(R, so.xpos.detach(), so.ypos.detach(), stride, stats=stats)
-    if training:   # folded into the unit tail's apply
-        sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2, defer=True)
+    if training:
+        sst = ops.bn_finalize(stats, B, Cout, To * V, mod.bn2)
     else:
         sst = ops.bn_eval_coef(mod.bn2, Cout)
     s = TcnSaved()
@@ -602,8 +552,8 @@ def convbn_core_forward(mod, x, training):
     To = (T - 1) // s_t + 1
     Rc = _empty(B, Cout, To, V, like=x)
     ops.pw_fwd(conv.weight, False, conv.bias, PV(x, s_t), PV(Rc), Cout, Cin, To, V)
-    if training:   # folded into the unit tail's apply
-        rst = ops.bn_finalize(ops.moments(Rc, False), B, Cout, To * V, bn, defer=True)
+    if training:
+        rst = ops.bn_finalize(ops.moments(Rc, False), B, Cout, To * V, bn)
     else:
         rst = ops.bn_eval_coef(bn, Cout)
     s = ConvBnSaved()
@@ -629,7 +579,7 @@ def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate, off=False):
 # TCN_GCN_unit
 # ======================================================================================
 class UnitSaved:
-    __slots__ = ("x", "gs", "ts", "rs", "out", "prev", "off")
+    __slots__ = ("x", "gs", "ts", "rs", "out", "prev", "off", "shared", "__weakref__")
 
 
 def unit_forward(unit, x, training):
@@ -638,21 +588,19 @@ def unit_forward(unit, x, training):
             x.shape[2] * x.shape[3] <= ops.TAIL_MAX_PLANE):
         # inference (no backward can follow): the Shift_gcn tail is fused into shift_in,
         # the unit tail into shift_out; neither H nor S is written
-        H = pre = None
-        if EVAL_GCN_EPI:   # the Shift_gcn tail in its contraction's epilogue
-            H = gcn_infer_h(unit.gcn1, x)
-        else:              # ... in the shift_in launch's staging (round-1 form)
-            pre = gcn_infer_z(unit.gcn1, x)
+        # the Shift_gcn tail (BN1d eval + down/identity + ReLU) is formed in the shift_in
+        # launch's staging
+        pre = gcn_infer_z(unit.gcn1, x)
         r = rst = None
         if unit.residual_kind == "conv":
-            if EVAL_FOLD or EVAL_GCN_EPI:
+            if EVAL_FOLD:
                 r = convbn_infer_folded(unit.residual, x)
             else:
                 r, rst, _ = convbn_core_forward(unit.residual, x, training)
         elif unit.residual_kind == "identity":
             r = x
         gm = _mask_of(consumer) if consumer is not None else None
-        out, xg_next = tcn_core_forward(unit.tcn1, H, training, tail=(r, rst, gm),
+        out, xg_next = tcn_core_forward(unit.tcn1, None, training, tail=(r, rst, gm),
                                         pre=pre)
         if gm is not None:
             consumer.__dict__["_gather_cache"] = (out, xg_next, gm)
@@ -710,6 +658,7 @@ def unit_forward(unit, x, training):
     s = UnitSaved()
     s.x, s.gs, s.ts, s.rs, s.out, s.prev = x, gs, ts, rs, out, prev
     s.off = off
+    _register(unit, s)
     return out, s
 
 
@@ -740,7 +689,7 @@ def _off_path_ok(unit, s: UnitSaved):
     """Weight gradients may run on the side stream only if autograd will take the returned
     gradient tensors as they are (every .grad is None, so AccumulateGrad stores them
     without launching anything on the current stream before the join)."""
-    if not s.off or torch.cuda.is_current_stream_capturing():
+    if not s.off or torch.cuda.is_current_stream_capturing() or s.shared:
         return False
     if torch.is_grad_enabled():
         # backward(create_graph=True): AccumulateGrad clones the gradient on the current
@@ -776,9 +725,8 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
                                         rst=s.rs.rst)
     else:
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False)
-    # (folded into its consumer: the shift_out backward, or the bn2/residual apply)
     coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
-        part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2, defer=True)
+        part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
     if kind != "conv" and so.stride == 1 and ops.ra_fits(To * V, V):
         # neither dS nor the identity-residual gradient is written: the shift_out backward
         # forms dS while staging, gcn_dx_finish forms dout*(out > 0)
@@ -800,7 +748,7 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
     dres = None
     if kind == "conv":
         coefR, g["residual.bn.weight"], g["residual.bn.bias"] = ops.bn_bwd_finalize(
-            rpart, B, Cout, B * To * V, s.rs.rst, unit.residual.bn, defer=True)
+            rpart, B, Cout, B * To * V, s.rs.rst, unit.residual.bn)
         dres = torch.empty_like(s.rs.Rc)
         ops.bn_bwd_apply(dout, s.out, True, S, coef2, False, r=s.rs.Rc, rcoef=coefR, dr=dres,
                          dx=dS)
@@ -838,19 +786,10 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
 # two-launch form is faster at C = 256 too (+0.5 % same-box, profiles/r03_tsh/), so by
 # default no unit fuses (512 exceeds every Shift-GCN width). A/B knob (0 = every unit).
 TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "512"))
-# Inference (no backward possible, eval mode) unit recipe, round 4: 1 = the Shift_gcn tail
-# (BatchNorm1d eval + down with its BatchNorm folded / identity + ReLU) in the gcn
-# contraction's epilogue (sgcn_pw_fwd_bn_res) and the residual tcn's BatchNorm folded into
-# its conv; 0 = the round-1 form (Z stored, the tail formed in the shift_in launch). A/B knob.
-EVAL_GCN_EPI = int(os.environ.get("SGCN_EVAL_GCN_EPI", "0"))
 # Inference: the eval-mode BatchNorm right after a conv (down.1 after down.0, residual.bn
 # after residual.conv) folded into that conv's weights and bias (folded_conv_bn), so the
 # consumer adds the residual without an affine. A/B knob (round 4).
 EVAL_FOLD = int(os.environ.get("SGCN_EVAL_FOLD", "1"))
-# Inference: Shift_tcn's shift_in (+ bn eval affine) formed inside temporal_linear's operand
-# staging (sgcn_pw_fwd_tshift, no side output) from this many input channels up; needs
-# EVAL_GCN_EPI (H materialised). A/B knob.
-EVAL_TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_EVAL_TSHIFT_FUSION_MIN_C", "512"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
 # (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass: 2 = every unit (with a
 # down conv, the down BatchNorm's sums too; round 3), 1 = units without a down conv only
@@ -861,10 +800,6 @@ GBN_FUSION = int(os.environ.get("SGCN_GBN_FUSION", "2"))
 # gradient finalizes, the next unit's mask and the forward's down / residual conv branches.
 # SGCN_ASYNC_DW=0 serializes everything (bench.py's roofline steps, A/B).
 ASYNC_DW = int(os.environ.get("SGCN_ASYNC_DW", "1"))
-# The side stream on a CU-masked HIP stream of this many CUs (0 = an ordinary stream, all
-# CUs), chosen by SGCN_SIDE_CU_PATTERN (low / high / spread). A/B knob (round 4).
-SIDE_CUS = int(os.environ.get("SGCN_SIDE_CUS", "0"))
-SIDE_CU_PATTERN = os.environ.get("SGCN_SIDE_CU_PATTERN", "low")
 
 
 def trainable(module):
@@ -943,7 +878,7 @@ def _tcn_standalone_bwd(mod, ts, dy):
     S = ts.S
     B, C, To, V = S.shape
     part, _ = ops.bn_bwd_reduce(dy, None, False, S, ts.sst, False)
-    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, ts.sst, mod.bn2, defer=True)
+    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, ts.sst, mod.bn2)
     dS = ops.bn_bwd_apply(dy, None, False, S, coef, False)
     dH, g = tcn_core_backward(mod, ts, dS)
     g["bn2.weight"], g["bn2.bias"] = dg, db
@@ -958,7 +893,7 @@ def _convbn_standalone_fwd(mod, x, training):
 def _convbn_standalone_bwd(mod, s, dy):
     B, C, To, V = s.Rc.shape
     part, _ = ops.bn_bwd_reduce(dy, None, False, s.Rc, s.rst, False)
-    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, s.rst, mod.bn, defer=True)
+    coef, dg, db = ops.bn_bwd_finalize(part, B, C, B * To * V, s.rst, mod.bn)
     dRc = ops.bn_bwd_apply(dy, None, False, s.Rc, coef, False)
     dx = torch.zeros_like(s.x)
     g = convbn_dx_and_dw(mod, s, dRc, dx, accumulate=True)

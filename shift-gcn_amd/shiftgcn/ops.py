@@ -19,64 +19,7 @@ _F32 = torch.float32
 def _ptr(t):
     if t is None:
         return None
-    if isinstance(t, PendingCoef):   # read as a tensor: its finalize launches first
-        t = t.tensor()
     return t.data_ptr()
-
-
-class BnBwdFoldStruct(ctypes.Structure):
-    """``sgcn_bn_bwd_fold`` (include/shiftgcn.h)."""
-    _fields_ = [("part", ctypes.c_void_p), ("mean", ctypes.c_void_p),
-                ("invstd", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
-                ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
-                ("coef", ctypes.c_void_p), ("n_total", ctypes.c_double),
-                ("batch_stats", ctypes.c_int)]
-
-
-class PendingCoef:
-    """A per-channel BatchNorm backward finalize left for its consumer to fold (round 4,
-    ``bn_bwd_finalize(..., defer=True)``): ``take_fold()`` hands it to a folding consumer
-    (sgcn_tshift_bwd_bnin_fold, sgcn_bn_bwd_apply_fold), whose plane workgroups write the
-    coefficients and dgamma/dbeta; ``tensor()`` (or any other use) launches
-    sgcn_bn_bwd_finalize first."""
-
-    __slots__ = ("t", "_spec")
-
-    def __init__(self, coef, spec):
-        self.t, self._spec = coef, spec
-
-    @property
-    def pending(self):
-        return self._spec is not None
-
-    def tensor(self):
-        spec, self._spec = self._spec, None
-        if spec is not None:
-            part, B, F, n_total, st, bn, dgamma, dbeta = spec
-            part.record_stream(torch.cuda.current_stream(part.device))
-            with _timed("finalize", 0, 4 * part.numel(), part):
-                rc = _lib.load().sgcn_bn_bwd_finalize(
-                    _ptr(part), B, F, int(n_total), 0, _ptr(st.mean), _ptr(st.invstd),
-                    _ptr(bn.weight), _ptr(dgamma), _ptr(dbeta), 0, int(st.batch), _ptr(self.t),
-                    _stream(part))
-            _lib.check(rc, "sgcn_bn_bwd_finalize")
-        return self.t
-
-    def take_fold(self):
-        spec, self._spec = self._spec, None
-        if spec is None:
-            return None
-        part, B, F, n_total, st, bn, dgamma, dbeta = spec
-        part.record_stream(torch.cuda.current_stream(part.device))
-        f = BnBwdFoldStruct(_ptr(part), _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
-                            _ptr(dgamma), _ptr(dbeta), _ptr(self.t), float(n_total),
-                            int(st.batch))
-        return f, part
-
-
-def _fold_of(c):
-    """(struct, keep) if ``c`` is a pending backward finalize, else None."""
-    return c.take_fold() if isinstance(c, PendingCoef) and c.pending else None
 
 
 # --------------------------------------------------------------------------------------
@@ -193,14 +136,71 @@ def grad_slot(p):
     return flat[off:off + p.numel()].view(p.shape)
 
 
+# slots handed out since the bucket's last release (GradAllReduce.__call__): a slot goes to
+# at most ONE gradient tensor per backward. A parameter with two gradient contributions in
+# one backward (the model called twice before one backward), or two torch.autograd.grad
+# calls, would otherwise get the same memory twice: the second kernel would overwrite the
+# first contribution before autograd sums them.
+_SLOT_TAKEN = WeakIdKeyDictionary()
+
+
+def release_grad_slots(params):
+    """Make the slots of ``params`` available to the next backward."""
+    for p in params:
+        _SLOT_TAKEN.pop(p, None)
+
+
 def grad_like(p):
-    """Output tensor for p's gradient: its bucket slot while p.grad is None, else a new
-    tensor like p."""
-    if p.grad is None:
+    """Output tensor for p's gradient: its bucket slot while p.grad is None and the slot was
+    not handed out yet since the last release, else a new tensor like p."""
+    if p.grad is None and p not in _SLOT_TAKEN:
         v = grad_slot(p)
         if v is not None:
+            _SLOT_TAKEN[p] = True
             return v
     return torch.empty_like(p)
+
+
+def bump_versions(tensors):
+    """Advance the autograd version counters of tensors a HIP kernel wrote in place through
+    a raw pointer (torch cannot see those writes): anything keyed on ``_version`` — the
+    eval-mode caches below, fused.folded_conv_bn, autograd's saved-tensor checks — then
+    sees the change."""
+    ts = [t for t in tensors if t is not None]
+    if ts:
+        torch.autograd.graph.increment_version(ts)
+
+
+def _src_key(tensors):
+    return tuple((t.data_ptr(), t._version) if t is not None else None for t in tensors)
+
+
+def _cache_tensors(v):
+    if isinstance(v, BnStats):
+        return (v.buf,)
+    if isinstance(v, torch.Tensor):
+        return (v,)
+    return tuple(t for x in v for t in _cache_tensors(x))
+
+
+def cached(owner, slot, key, make, device):
+    """Value computed by ``make()`` once per ``key`` (storage + version of every tensor it
+    reads), kept in ``owner.__dict__[slot]``: the eval-mode constants (BatchNorm apply
+    coefficients, tanh(Feature_Mask) + 1) that change only when a weight or running
+    statistic does. A stream that reads a cached tensor other than the one that made it is
+    recorded on it (the caching allocator then keeps its memory until that stream is done
+    when the entry is replaced)."""
+    c = owner.__dict__.get(slot)
+    cur = torch.cuda.current_stream(device)
+    if c is not None and c[0] == key:
+        if cur not in c[2] and not torch.cuda.is_current_stream_capturing():
+            for t in _cache_tensors(c[1]):
+                t.record_stream(cur)
+            c[2].add(cur)
+        return c[1]
+    v = make()
+    owner.__dict__[slot] = (key, v, {cur})
+    return v
 
 
 def _stream(t: torch.Tensor):
@@ -231,16 +231,12 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
                ypos_is_raw=True, affine=None):
     """Forward shift of ``inp`` (B,C,H,W) -> (B,C,H//stride,W). ``ypos`` is the RAW
     parameter (the +0.5 for stride != 1 is applied in-kernel). Optional fused
-    per-channel input affine (scale, shift) — or ``affine``, a BnStats whose pending
-    finalize the shift folds (sgcn_tshift_fwd_fold) — and per-plane output moments
+    per-channel input affine (scale, shift) — or ``affine``, a BnStats supplying them — and
+    per-plane output moments
     ``stats`` (B*C*2 floats). float64 tensors run the double-precision kernel (no fused
     options)."""
     if affine is not None:
-        fold = affine.take_fold()
-        if fold is None:
-            scale, shift = affine.scale, affine.shift
-        else:
-            return _tshift_fwd_fold(inp, xpos, ypos, stride, fold, stats, out, ypos_is_raw)
+        scale, shift = affine.scale, affine.shift
     if inp.dtype == torch.float64:
         if scale is not None or shift is not None or stats is not None:
             raise RuntimeError("the fused shift options are float32-only")
@@ -259,24 +255,6 @@ def tshift_fwd(inp, xpos, ypos, stride, scale=None, shift=None, stats=None, out=
                                  _ptr(shift), _ptr(stats), B, C, H, W, stride,
                                  int(ypos_is_raw), _stream(inp))
     _lib.check(rc, "sgcn_tshift_fwd")
-    return out
-
-
-def _tshift_fwd_fold(inp, xpos, ypos, stride, fold, stats, out, ypos_is_raw):
-    check_input(inp, "input")
-    check_input(xpos, "xpos")
-    check_input(ypos, "ypos")
-    _opt(stats, "stats")
-    B, C, H, W = inp.shape
-    if out is None:
-        out = torch.empty((B, C, H // stride, W), device=inp.device, dtype=_F32)
-    f, _keep = fold
-    nb = 4 * (inp.numel() + out.numel())
-    with _timed("tshift_fwd", 0, nb, inp, "FOLD " + _shp(inp)):
-        rc = _lib.load().sgcn_tshift_fwd_fold(_ptr(inp), _ptr(out), _ptr(xpos), _ptr(ypos),
-                                              ctypes.byref(f), _ptr(stats), B, C, H, W, stride,
-                                              int(ypos_is_raw), _stream(inp))
-    _lib.check(rc, "sgcn_tshift_fwd_fold")
     return out
 
 
@@ -499,12 +477,8 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False, pos_out=No
     """Stride-1 shift backward (ReLU mask on ``inp``) whose output gradient is the input
     gradient of the following BatchNorm, k1*(y > 0 ? dy : 0) + k2*s + k3 (s = that
     BatchNorm's input), formed in the kernel. Returns (grad_input, grad_xpos, grad_ypos)."""
-    fold = _fold_of(coef)
-    for t, n in ((dy, "dy"), (y, "y"), (s, "s"), (inp, "input")):
+    for t, n in ((dy, "dy"), (y, "y"), (s, "s"), (inp, "input"), (coef, "coef")):
         check_input(t, n)
-    if fold is None:
-        coef = coef.tensor() if isinstance(coef, PendingCoef) else coef
-        check_input(coef, "coef")
     B, C, H, W = inp.shape
     lib = _lib.load()
     dev = inp.device
@@ -514,11 +488,10 @@ def tshift_bwd_bnin(dy, y, s, coef, inp, xpos, ypos, defer_pos=False, pos_out=No
     gx, gy, pp = _pos_out(defer_pos, ws, B, C, dev, pos_out)
     nb = 4 * (3 * dy.numel() + 2 * inp.numel())
     with _timed("tshift_bwd", 0, nb, inp, _shp(inp)):
-        rc = lib.sgcn_tshift_bwd_bnin_fold(
-            _ptr(dy), _ptr(y), _ptr(s), None if fold else _ptr(coef),
-            ctypes.byref(fold[0]) if fold else None, _ptr(inp), _ptr(xpos), _ptr(ypos),
+        rc = lib.sgcn_tshift_bwd_bnin(
+            _ptr(dy), _ptr(y), _ptr(s), _ptr(coef), _ptr(inp), _ptr(xpos), _ptr(ypos),
             _ptr(gin), _ptr(gx), _ptr(gy), _ptr(ws), nbytes, B, C, H, W, 1, _stream(inp))
-    _lib.check(rc, "sgcn_tshift_bwd_bnin_fold")
+    _lib.check(rc, "sgcn_tshift_bwd_bnin")
     return gin, (pp if pp is not None else gx), gy
 
 
@@ -616,36 +589,6 @@ def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=Fals
     return dw
 
 
-def pw_fwd_bn_res(w, w_mcontig, bias, x: PlaneView, st, res, out: PlaneView, M, K, T, V):
-    """Inference Shift_gcn (sgcn_pw_fwd_bn_res): out = relu((w @ x + bias) * st.scale +
-    st.shift + res) with the per-(channel, stored joint) eval coefficients of its
-    BatchNorm1d(V*C) (``st`` from bn_eval_coef(..., perm_V=V)) and the residual ``res``
-    (out's layout) read at the stored address."""
-    check_input(w, "weight")
-    _opt(bias, "bias")
-    check_input(res, "residual")
-    if x.tstride != 1 or x.rsign != 0 or out.tstride != 1:
-        raise ValueError("pw_fwd_bn_res: plain input planes, unit time stride")
-    if res.shape != out.t.shape or res.stride() != out.t.stride():
-        raise ValueError("pw_fwd_bn_res: the residual must have the output's layout")
-    B = x.t.shape[0]
-    lib = _lib.load()
-    P = B * T * V
-    bc = _batch_chunk([(x, K), (out, M)], B, T, V)
-    with _timed("pw_fwd", 2.0 * P * M * K, 4.0 * P * (2 * M + K), x.t,
-                f"EPI M{M} K{K} T{T} V{V} yrot{out.rsign} mc{int(w_mcontig)}"):
-        for b0 in range(0, B, bc):
-            nb = min(bc, B - b0)
-            rc = lib.sgcn_pw_fwd_bn_res(_ptr(w), int(w_mcontig), _ptr(bias),
-                                        x.t.data_ptr() + 4 * b0 * x.bstride, x.bstride,
-                                        x.cstride, _ptr(st.scale), _ptr(st.shift),
-                                        res.data_ptr() + 4 * b0 * out.bstride,
-                                        out.t.data_ptr() + 4 * b0 * out.bstride, out.bstride,
-                                        out.cstride, out.rsign, nb, M, K, T, V, _stream(x.t))
-            _lib.check(rc, "sgcn_pw_fwd_bn_res")
-    return out.t
-
-
 def pw_fwd_tshift(w, bias, x: PlaneView, xpos, ypos, st, out: PlaneView, M, K, T, V,
                   relu=False, x_shifted=None):
     """Shift_tcn's shift_in fused into temporal_linear (sgcn_pw_fwd_tshift):
@@ -698,133 +641,53 @@ def moments(x, per_joint):
     return part
 
 
-class BnFoldStruct(ctypes.Structure):
-    """``sgcn_bn_fold`` (include/shiftgcn.h): a training BatchNorm finalize folded into its
-    first consumer's prologue."""
-    _fields_ = [("part", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
-                ("beta", ctypes.c_void_p), ("running_mean", ctypes.c_void_p),
-                ("running_var", ctypes.c_void_p), ("num_batches", ctypes.c_void_p),
-                ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
-                ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p),
-                ("n_part", ctypes.c_int), ("eps", ctypes.c_float),
-                ("momentum", ctypes.c_float)]
-
-
 class BnStats:
     """Statistics and apply coefficients of one BatchNorm call (local feature order):
-    batch statistics in training mode, running statistics in eval mode (``batch``).
+    batch statistics in training mode, running statistics in eval mode (``batch``)."""
 
-    A training-mode per-channel finalize may be left PENDING (``bn_finalize(...,
-    defer=True)``, round 4): a consumer that folds it (sgcn_tshift_fwd_fold,
-    sgcn_bn_apply_fold) takes it with :meth:`take_fold` and its plane workgroups compute the
-    coefficients; anything else that reads ``mean``/``invstd``/``scale``/``shift`` first
-    launches the finalize (:meth:`resolve`), on the current stream."""
-
-    __slots__ = ("_mean", "_invstd", "_scale", "_shift", "_buf", "batch", "_pending")
+    __slots__ = ("mean", "invstd", "scale", "shift", "buf", "batch")
 
     def __init__(self, F, device, batch=True):
         buf = torch.empty((4, F), device=device, dtype=_F32)
-        self._buf = buf
-        self._mean, self._invstd, self._scale, self._shift = buf[0], buf[1], buf[2], buf[3]
+        self.buf = buf
+        self.mean, self.invstd, self.scale, self.shift = buf[0], buf[1], buf[2], buf[3]
         self.batch = batch
-        self._pending = None
-
-    @property
-    def mean(self):
-        self.resolve()
-        return self._mean
-
-    @property
-    def invstd(self):
-        self.resolve()
-        return self._invstd
-
-    @property
-    def scale(self):
-        self.resolve()
-        return self._scale
-
-    @property
-    def shift(self):
-        self.resolve()
-        return self._shift
-
-    @property
-    def pending(self):
-        return self._pending is not None
-
-    def resolve(self):
-        """Launch the pending finalize (sgcn_bn_finalize), if any."""
-        p, self._pending = self._pending, None
-        if p is None:
-            return
-        part, B, F, n_part, bn, track = p
-        momentum = bn.momentum if bn.momentum is not None else 0.0
-        part.record_stream(torch.cuda.current_stream(part.device))
-        with _timed("finalize", 0, 4 * part.numel(), part):
-            rc = _lib.load().sgcn_bn_finalize(
-                _ptr(part), B, F, n_part, 0, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps),
-                float(momentum), _ptr(bn.running_mean) if track else None,
-                _ptr(bn.running_var) if track else None,
-                _ptr(bn.num_batches_tracked) if track else None, _ptr(self._mean),
-                _ptr(self._invstd), _ptr(self._scale), _ptr(self._shift), _stream(part))
-        _lib.check(rc, "sgcn_bn_finalize")
-
-    def take_fold(self):
-        """(ctypes struct, keep-alive) of the pending finalize for a folding consumer, which
-        then writes the statistics; None if nothing is pending."""
-        p, self._pending = self._pending, None
-        if p is None:
-            return None
-        part, B, F, n_part, bn, track = p
-        cur = torch.cuda.current_stream(part.device)
-        part.record_stream(cur)          # made (or allocated) on another stream
-        self._buf.record_stream(cur)
-        momentum = bn.momentum if bn.momentum is not None else 0.0
-        f = BnFoldStruct(_ptr(part), _ptr(bn.weight), _ptr(bn.bias),
-                         _ptr(bn.running_mean) if track else None,
-                         _ptr(bn.running_var) if track else None,
-                         _ptr(bn.num_batches_tracked) if track else None, _ptr(self._mean),
-                         _ptr(self._invstd), _ptr(self._scale), _ptr(self._shift),
-                         int(n_part), float(bn.eps), float(momentum))
-        return f, part
 
 
-# Per-channel training finalizes left pending for their consumer to fold (round 4, A/B knob
-# SGCN_FOLD_FINALIZE=1). Off by default: measured -1.4 % on the NTU step (the consumer's
-# 8,192 plane workgroups each gathering their channel's B partials, one cache line per
-# sample at the [sample][channel] stride, cost more than the 25 launches they remove;
-# profiles/r04_fold/).
-FOLD_FINALIZE = int(__import__("os").environ.get("SGCN_FOLD_FINALIZE", "0"))
-
-
-def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True, defer=False):
+def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
     """Training-mode statistics of ``bn`` (an nn.BatchNorm*d) from partials; updates its
-    running stats / num_batches_tracked exactly once, like ``bn.forward`` in train().
-    ``defer`` (per-channel only): leave the finalize pending in the returned BnStats for a
-    consumer to fold (BnStats.take_fold), or launched on first read."""
+    running stats / num_batches_tracked exactly once, like ``bn.forward`` in train()."""
     st = BnStats(F, part.device)
     lib = _lib.load()
     track = training and bn.track_running_stats and bn.running_mean is not None
     if track and bn.momentum is None:
         # the cumulative moving average (momentum=None) is never used by the reference
         raise NotImplementedError("BatchNorm momentum=None is not supported on the HIP path")
-    if defer and FOLD_FINALIZE and perm_V == 0:
-        st._pending = (part, B, F, n_part, bn, track)
-        return st
     momentum = bn.momentum if bn.momentum is not None else 0.0
     with _timed("finalize", 0, 4 * part.numel(), part):
         rc = lib.sgcn_bn_finalize(
             _ptr(part), B, F, n_part, perm_V, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps),
             float(momentum), _ptr(bn.running_mean) if track else None,
             _ptr(bn.running_var) if track else None,
-            _ptr(bn.num_batches_tracked) if track else None, _ptr(st._mean),
-            _ptr(st._invstd), _ptr(st._scale), _ptr(st._shift), _stream(part))
+            _ptr(bn.num_batches_tracked) if track else None, _ptr(st.mean),
+            _ptr(st.invstd), _ptr(st.scale), _ptr(st.shift), _stream(part))
     _lib.check(rc, "sgcn_bn_finalize")
+    if track:   # the running statistics were written in place by the kernel
+        bump_versions((bn.running_mean, bn.running_var, bn.num_batches_tracked))
     return st
 
 
 def bn_eval_coef(bn, F, perm_V=0, device=None):
+    """Eval-mode coefficients of ``bn`` (running statistics), computed once per version of
+    its weight, bias and running statistics (:func:`cached`; the training step's writers
+    bump those versions: FusedSGD, bn_finalize, broadcast_buffers)."""
+    key = _src_key((bn.weight, bn.bias, bn.running_mean, bn.running_var)) + (
+        float(bn.eps), F, perm_V)
+    return cached(bn, "_sgcn_eval_coef", key, lambda: _bn_eval_coef(bn, F, perm_V),
+                  bn.running_mean.device)
+
+
+def _bn_eval_coef(bn, F, perm_V):
     st = BnStats(F, bn.running_mean.device, batch=False)
     with _timed("finalize", 0, 4 * 8 * F, bn.running_mean):
         rc = _lib.load().sgcn_bn_eval_coef(F, perm_V, _ptr(bn.weight), _ptr(bn.bias),
@@ -848,20 +711,13 @@ def bn_apply(x, st: BnStats, per_joint, r=None, rst: BnStats = None, relu=False,
     ys = torch.empty((B * C * 2,), device=x.device, dtype=_F32) if out_stats else None
     yg = torch.empty_like(y) if gather_m is not None else None
     nb = 4 * x.numel() * (2 + (r is not None) + (yg is not None))
-    # pending per-channel finalizes are folded into this launch (sgcn_bn_apply_fold)
-    fm = st.take_fold() if (not per_joint and st.pending) else None
-    fr = rst.take_fold() if (rst is not None and rst.pending) else None
-    sc = st._scale if fm is not None else st.scale
-    sh = st._shift if fm is not None else st.shift
-    with _timed("bn_apply", 0, nb, x, ("FOLD " if fm or fr else "") + _shp(x)):
-        rc = _lib.load().sgcn_bn_apply_fold(
-            _ptr(x), _ptr(sc), _ptr(sh), int(per_joint),
-            ctypes.byref(fm[0]) if fm is not None else None, _ptr(r),
-            _ptr(rst.scale) if (rst is not None and fr is None) else None,
-            _ptr(rst.shift) if (rst is not None and fr is None) else None,
-            ctypes.byref(fr[0]) if fr is not None else None, int(relu), _ptr(y), _ptr(ys),
+    with _timed("bn_apply", 0, nb, x, _shp(x)):
+        rc = _lib.load().sgcn_bn_apply(
+            _ptr(x), _ptr(st.scale), _ptr(st.shift), int(per_joint), _ptr(r),
+            _ptr(rst.scale) if rst is not None else None,
+            _ptr(rst.shift) if rst is not None else None, int(relu), _ptr(y), _ptr(ys),
             _ptr(gather_m), _ptr(yg), B, C, T, V, _stream(x))
-    _lib.check(rc, "sgcn_bn_apply_fold")
+    _lib.check(rc, "sgcn_bn_apply")
     if gather_m is not None:
         return y, yg
     return y if out_stats is None else (y, ys)
@@ -885,16 +741,12 @@ def bn_bwd_reduce(dy, y, relu, x, st: BnStats, per_joint, r=None, rst: BnStats =
     return part, rpart
 
 
-def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0, defer=False):
-    """Returns (coef[3,F], dgamma, dbeta) with dgamma/dbeta in the module's layout.
-    ``defer`` (per-channel only): coef is a PendingCoef that its consumer folds (dgamma /
-    dbeta are then written by that consumer's launch)."""
+def bn_bwd_finalize(part, B, F, n_total, st: BnStats, bn, perm_V=0):
+    """Returns (coef[3,F], dgamma, dbeta) with dgamma/dbeta in the module's layout."""
     dev = part.device
     coef = torch.empty((3, F), device=dev, dtype=_F32)
     dgamma = grad_like(bn.weight) if bn.weight is not None else None
     dbeta = grad_like(bn.bias) if bn.bias is not None else None
-    if defer and FOLD_FINALIZE and perm_V == 0:
-        return PendingCoef(coef, (part, B, F, n_total, st, bn, dgamma, dbeta)), dgamma, dbeta
     with _timed("finalize", 0, 4 * part.numel(), part):
         rc = _lib.load().sgcn_bn_bwd_finalize(_ptr(part), B, F, int(n_total), perm_V,
                                               _ptr(st.mean), _ptr(st.invstd), _ptr(bn.weight),
@@ -927,16 +779,11 @@ def bn_bwd_apply(dy, y, relu, x, coef, per_joint, r=None, rcoef=None, dr=None, d
     B, C, T, V = x.shape
     dx = torch.empty_like(x) if dx is None else dx
     nb = 4 * x.numel() * (3 + (y is not None) + (r is not None) + (dr is not None))
-    # pending per-channel backward finalizes are folded into this launch
-    fm = _fold_of(coef) if not per_joint else None
-    fr = _fold_of(rcoef)
-    with _timed("bn_bwd_apply", 0, nb, x, ("FOLD " if fm or fr else "") + _shp(x)):
-        rc = _lib.load().sgcn_bn_bwd_apply_fold(
-            _ptr(dy), _ptr(y), int(relu), _ptr(x), None if fm else _ptr(coef), int(per_joint),
-            ctypes.byref(fm[0]) if fm else None, _ptr(r), None if fr else _ptr(rcoef),
-            ctypes.byref(fr[0]) if fr else None, _ptr(dy_coef), _ptr(dx), _ptr(dr), B, C, T,
-            V, _stream(x))
-    _lib.check(rc, "sgcn_bn_bwd_apply_fold")
+    with _timed("bn_bwd_apply", 0, nb, x, _shp(x)):
+        rc = _lib.load().sgcn_bn_bwd_apply(
+            _ptr(dy), _ptr(y), int(relu), _ptr(x), _ptr(coef), int(per_joint), _ptr(r),
+            _ptr(rcoef), _ptr(dy_coef), _ptr(dx), _ptr(dr), B, C, T, V, _stream(x))
+    _lib.check(rc, "sgcn_bn_bwd_apply")
     return dx
 
 

@@ -104,7 +104,7 @@ class FusedSGD(torch.optim.SGD):
         import struct
 
         from . import _lib
-        from .ops import _stream
+        from .ops import _stream, bump_versions
         lib = _lib.load()
         g0 = self.param_groups[0]
         momentum = float(g0["momentum"])
@@ -143,6 +143,13 @@ class FusedSGD(torch.optim.SGD):
         rc = lib.sgcn_sgd_step(table.data_ptr(), numel_d.data_ptr(), chunks_d.data_ptr(),
                                nchunks, momentum, int(bool(g0["nesterov"])), _stream(table))
         _lib.check(rc, "sgcn_sgd_step")
+        # the kernel wrote every parameter, momentum buffer and scaled gradient in place:
+        # advance their version counters as torch's own in-place update would
+        written = [p for p, _ in items]
+        if momentum != 0:
+            written += [self.state[p]["momentum_buffer"] for p in written]
+        written += [p.grad for p, _ in items if id(p) in gscale]
+        bump_versions(written)
         return loss
 
 

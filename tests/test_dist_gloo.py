@@ -246,3 +246,68 @@ def test_deferred_scale_matches_multiply_then_step_gloo_world2():
             other = True if key is False else (True, "grad")
             for n, v in out[key].items():
                 assert np.array_equal(v, out[other][n]), (rank, key, n)
+
+
+def _clip_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    torch.set_num_threads(1)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shiftgcn.dist import GradAllReduce, broadcast_parameters
+        from shiftgcn.train import FusedSGD
+        out = {}
+        for defer in (False, True):
+            torch.manual_seed(5)
+            m = Toy()
+            broadcast_parameters(m)
+            opt = (FusedSGD if defer else torch.optim.SGD)(
+                [p for p in m.parameters() if p.requires_grad], lr=0.1, momentum=0.9,
+                nesterov=True, weight_decay=1e-4)
+            ga = GradAllReduce(m, defer_scale_to=opt if defer else None)
+            g = torch.Generator().manual_seed(7 + rank)
+            for p in m.parameters():
+                if p.requires_grad:
+                    p.grad = 3.0 * torch.randn(p.shape, generator=g)
+            ga()
+            out[(defer, "norm")] = float(ga.clip_grad_norm_(0.5))
+            opt.step()
+            ga.close()
+            out[defer] = {n: p.detach().numpy().copy() for n, p in m.named_parameters()
+                          if p.requires_grad}
+        # reference: reduce by hand, clip with torch, step
+        torch.manual_seed(5)
+        m = Toy()
+        broadcast_parameters(m)
+        opt = torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=0.1,
+                              momentum=0.9, nesterov=True, weight_decay=1e-4)
+        g = torch.Generator().manual_seed(7 + rank)
+        for n, p in m.named_parameters():
+            if p.requires_grad:
+                p.grad = 3.0 * torch.randn(p.shape, generator=g)
+                dist.all_reduce(p.grad)
+                if not (n.endswith(".xpos") or n.endswith(".ypos")):
+                    p.grad.mul_(1.0 / world)
+        out["torch_norm"] = float(torch.nn.utils.clip_grad_norm_(
+            [p for p in m.parameters() if p.requires_grad], 0.5))
+        opt.step()
+        out["torch"] = {n: p.detach().numpy().copy() for n, p in m.named_parameters()
+                        if p.requires_grad}
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_clip_grad_norm_in_both_scale_forms_gloo_world2():
+    """ADVICE r04: with the deferred scale, .grad holds the rank SUM until step();
+    GradAllReduce.clip_grad_norm_ clips the REDUCED gradients in both forms, matching
+    torch.nn.utils.clip_grad_norm_ over the reduced .grad followed by torch's SGD."""
+    res = _spawn(_clip_worker)
+    for rank, out in res:
+        for defer in (False, True):
+            assert abs(out[(defer, "norm")] - out["torch_norm"]) <= 1e-5 * out["torch_norm"]
+            for n, v in out[defer].items():
+                np.testing.assert_allclose(v, out["torch"][n], rtol=1e-6, atol=1e-7,
+                                           err_msg=f"{rank} {defer} {n}")

@@ -114,20 +114,25 @@ def test_two_shard_hip_passes_match_dataparallel_emulation():
 
 
 def test_bench_two_ranks_same_device():
-    """bench.py's N=2 path (torchrun, one process per rank, GradAllReduce after backward,
-    max-over-ranks timing, rank 0 prints) on one GPU with a gloo all-reduce. Guards the
+    """``bench.py --gpus 2`` with no launcher starts its two ranks itself (one process per
+    rank, GradAllReduce after backward, max-over-ranks timing, rank 0 prints) — here both on
+    cuda:0 with a gloo all-reduce. The line records the process group torch.distributed
+    reports (world size, backend) and every rank's ms per step. Also guards the
     rank-0-only-loop deadlock found in round 1 (every rank must run the roofline steps)."""
     env = dict(os.environ, SGCN_BENCH_BACKEND="gloo", SGCN_BENCH_SAME_DEVICE="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29517", os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "4",
-           "--cpu-baseline", "0"]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--batch", "4", "--cpu-baseline", "0"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 8 and d["value"] > 0
+    assert d["config"]["world_size"] == 2 and d["config"]["backend"] == "gloo"
+    rm = d["config"]["rank_ms_per_step"]
+    assert len(rm) == 2 and abs(max(rm) - d["ms_per_step"]) < 1e-2, (rm, d["ms_per_step"])
 
 
 def _free_port():

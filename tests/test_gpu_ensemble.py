@@ -93,10 +93,31 @@ def test_ensemble_graph_replay_matches_eager():
         assert torch.equal(s_g, s_eager) and torch.equal(l_g, l_eager)
 
 
-# inference recipes (shiftgcn.fused knobs): (EVAL_GCN_EPI, EVAL_TSHIFT_FUSION_MIN_C)
-# (EVAL_GCN_EPI, EVAL_TSHIFT_FUSION_MIN_C, EVAL_FOLD)
-RECIPES = {"pre-staged": (0, 512, 0), "pre-staged+fold": (0, 512, 1),
-           "gcn-epilogue": (1, 512, 1), "epilogue+tshift-fused": (1, 0, 1)}
+def test_ensemble_graph_recaptures_after_weight_change():
+    """EnsembleGraph holds no eval-constant launches (they are cached per weight version
+    outside the graph): after an in-place weight or running-statistics change, run()
+    captures again and still matches the eager forward."""
+    e = _our_ensemble()
+    from shiftgcn.ensemble import EnsembleGraph
+    x = formula.tensor((4, 3, 32, 33, 1), 903, 1.0).to(DEV)
+    g = EnsembleGraph(e, x.shape, DEV)
+    s0, _ = g.run(x)
+    s0 = s0.clone()
+    assert g.captures == 1
+    with torch.no_grad():
+        e.models[2].l3.gcn1.bn.running_var.mul_(2.0)
+        e.models[1].l5.tcn1.temporal_linear.weight.mul_(-1.0)
+        e.models[0].data_bn.running_mean.add_(0.5)
+    s1, l1 = g.run(x)
+    se, le = e(x)
+    torch.cuda.synchronize()
+    assert g.captures == 2
+    assert torch.equal(s1, se) and torch.equal(l1, le)
+    assert not torch.equal(s0, s1)
+
+
+# inference recipes (shiftgcn.fused knob EVAL_FOLD)
+RECIPES = {"pre-staged": 0, "pre-staged+fold": 1}
 
 
 @pytest.mark.parametrize("recipe", list(RECIPES))
@@ -106,17 +127,12 @@ RECIPES = {"pre-staged": (0, 512, 0), "pre-staged+fold": (0, 512, 1),
                                                         (128, 256, 2, True, 33)])
 def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V, recipe,
                                              monkeypatch):
-    """The no-backward recipes (round 1: Shift_gcn tail staged into shift_in; round 4: that
-    tail in the gcn contraction's epilogue with the down / residual BatchNorms folded into
-    their convs, optionally shift_in formed inside temporal_linear's staging; always the unit
-    tail in the shift_out store and the next-unit gather) equal the eval recipe a backward
-    would use."""
+    """The no-backward recipe (the Shift_gcn tail staged into shift_in, the unit tail in the
+    shift_out store and the next-unit gather; optionally the down / residual BatchNorms
+    folded into their convs) equals the eval recipe a backward would use."""
     import shiftgcn
     from shiftgcn import fused
-    epi, minc, fold = RECIPES[recipe]
-    monkeypatch.setattr(fused, "EVAL_GCN_EPI", epi)
-    monkeypatch.setattr(fused, "EVAL_TSHIFT_FUSION_MIN_C", minc)
-    monkeypatch.setattr(fused, "EVAL_FOLD", fold)
+    monkeypatch.setattr(fused, "EVAL_FOLD", RECIPES[recipe])
     torch.manual_seed(3)
     u = shiftgcn.TCN_GCN_unit(cin, cout, None, stride=stride, residual=residual,
                               num_point=V)
@@ -131,11 +147,11 @@ def test_inference_fusions_match_eval_recipe(cin, cout, stride, residual, V, rec
     assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
 
 
-@pytest.mark.parametrize("epi", [0, 1])
-def test_folded_conv_bn_tracks_parameter_and_statistics_updates(epi, monkeypatch):
-    """The eval fold of down.1 into down.0 (and residual.bn into residual.conv) is cached
-    per tensor version: in-place changes of the running statistics or of the conv weight
-    (optimizer steps, load_state_dict) are seen by the next inference call."""
+def test_eval_constants_track_parameter_and_statistics_updates(monkeypatch):
+    """The eval fold of down.1 into down.0 (and residual.bn into residual.conv), the eval
+    BatchNorm coefficients and the masks are cached per tensor version: in-place changes of
+    the running statistics, of a conv weight or of a Feature_Mask (optimizer steps,
+    load_state_dict) are seen by the next inference call."""
     import shiftgcn
     from shiftgcn import fused
     u = shiftgcn.TCN_GCN_unit(64, 128, None, stride=2, residual=True, num_point=25)
@@ -146,14 +162,18 @@ def test_folded_conv_bn_tracks_parameter_and_statistics_updates(epi, monkeypatch
     def check():
         with torch.no_grad():
             fast = u(x)
-        ref = u(x.clone().requires_grad_(True)).detach()
+        # the eval recipe on a fresh copy of the current state: no cached constants
+        v = shiftgcn.TCN_GCN_unit(64, 128, None, stride=2, residual=True, num_point=25)
+        v.load_state_dict(u.state_dict())
+        v = v.to(DEV).eval()
+        ref = v(x.clone().requires_grad_(True)).detach()
         err = (fast - ref).abs().max().item()
         assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
         return fast
 
-    monkeypatch.setattr(fused, "EVAL_GCN_EPI", epi)
     monkeypatch.setattr(fused, "EVAL_FOLD", 1)
     y0 = check()
+    assert "_sgcn_eval_coef" in u.tcn1.bn2.__dict__      # cached
     with torch.no_grad():
         u.gcn1.down[1].running_var.mul_(3.0)
         u.residual.bn.running_mean.add_(0.25)
@@ -161,37 +181,53 @@ def test_folded_conv_bn_tracks_parameter_and_statistics_updates(epi, monkeypatch
     assert not torch.equal(y0, y1)
     with torch.no_grad():
         u.gcn1.down[0].weight.mul_(-0.5)
-    check()
+    y2 = check()
+    with torch.no_grad():
+        u.tcn1.bn2.weight.mul_(0.5)
+        u.gcn1.bn.running_mean.add_(0.1)
+    y3 = check()
+    with torch.no_grad():
+        u.gcn1.Feature_Mask.add_(0.3)
+    y4 = check()
+    for a, b in ((y1, y2), (y2, y3), (y3, y4)):
+        assert not torch.equal(a, b)
 
 
-@pytest.mark.parametrize("M,K,T,V,rsign", [(64, 64, 20, 25, 1), (128, 64, 12, 33, 1),
-                                           (256, 128, 9, 25, 1), (64, 3, 7, 25, 0)])
-def test_pw_fwd_bn_res_matches_torch(M, K, T, V, rsign):
-    """sgcn_pw_fwd_bn_res vs an fp64 torch evaluation: relu((W x + b) * s[m, v'] + t[m, v']
-    + res) with v' the stored (shift_out-rotated) joint."""
-    from shiftgcn import ops
-    g = torch.Generator().manual_seed(M + K + T + V)
-    B = 3
-    x = torch.randn(B, K, T, V, generator=g)
-    w = torch.randn(K, M, generator=g) / K ** 0.5          # Linear_weight (C_in, C_out)
-    b = torch.randn(M, generator=g)
-    sc = torch.rand(M * V, generator=g) + 0.5
-    sh = torch.randn(M * V, generator=g)
-    res = torch.randn(B, M, T, V, generator=g)
+def test_eval_constants_follow_native_training_steps():
+    """the training step writes weights (FusedSGD's one launch) and
+    running statistics (sgcn_bn_finalize) through raw pointers; those writers advance the
+    tensors' version counters, so train epoch -> eval -> train epoch -> eval recomputes
+    every cached eval constant (fold, BatchNorm coefficients, masks)."""
+    import shiftgcn
+    from shiftgcn import train
+    torch.manual_seed(5)
+    m = shiftgcn.Model(num_class=10, num_point=25, num_person=2, graph="graph.ntu_rgb_d.Graph")
+    formula.fill_state(m, seed=9)
+    m = m.to(DEV)
+    opt = train.build_optimizer(m, base_lr=0.1)
+    assert isinstance(opt, train.FusedSGD)
+    x = formula.tensor((4, 3, 16, 25, 2), 10, 1.0).to(DEV)
+    lab = torch.arange(4, device=DEV) % 10
 
-    class St:
-        pass
-    st = St()
-    st.scale, st.shift = sc.to(DEV), sh.to(DEV)
-    y = torch.empty(B, M, T, V, device=DEV)
-    ops.pw_fwd_bn_res(w.to(DEV), True, b.to(DEV), ops.PlaneView(x.to(DEV)), st, res.to(DEV),
-                      ops.PlaneView(y, 1, rsign), M, K, T, V)
-    z = torch.einsum("bktv,km->bmtv", x.double(), w.double()) + b.double().view(1, M, 1, 1)
-    # store joint v' = (v + rsign*m) mod V
-    vv = (torch.arange(V).view(1, V) + rsign * torch.arange(M).view(M, 1)) % V   # [m, v]
-    zr = torch.zeros_like(z)
-    zr.scatter_(3, vv.view(1, M, 1, V).expand(B, M, T, V), z)
-    ref = torch.relu(zr * sc.double().view(1, M, 1, V) + sh.double().view(1, M, 1, V)
-                     + res.double())
-    err = (y.cpu().double() - ref).abs().max().item()
-    assert err <= 2e-5 * max(1.0, ref.abs().max().item()), err
+    def evaluate():
+        m.eval()
+        with torch.no_grad():
+            fast = m(x)
+        m.train()
+        # a fresh copy of the current state (no cached constants), same eval path
+        f = shiftgcn.Model(num_class=10, num_point=25, num_person=2,
+                           graph="graph.ntu_rgb_d.Graph")
+        f.load_state_dict(m.state_dict())
+        f = f.to(DEV).eval()
+        with torch.no_grad():
+            ref = f(x)
+        err = (fast - ref).abs().max().item()
+        assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
+        return fast
+
+    outs = []
+    for _ in range(3):
+        for _ in range(2):
+            train.train_step(m, opt, x, lab)
+        outs.append(evaluate())
+    assert not torch.equal(outs[0], outs[1]) and not torch.equal(outs[1], outs[2])

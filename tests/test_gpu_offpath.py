@@ -175,3 +175,138 @@ def test_create_graph_backward_stays_in_order():
     assert res[0].keys() == res[1].keys() and len(res[0]) > 100
     for n in res[0]:
         assert torch.equal(res[0][n], res[1][n]), n
+
+
+def test_post_accumulate_grad_hook_sees_finished_gradient():
+    """a ``register_post_accumulate_grad_hook`` on a Feature_Mask and on
+    a ypos reads ``.grad`` right after AccumulateGrad: those units must neither defer the
+    gradient write (side stream / end-of-backward batch) nor hand out an unwritten tensor.
+    The hooks see the finished gradients and the step equals the in-order path bit for
+    bit."""
+    from shiftgcn import fused
+    dev = torch.device("cuda:0")
+    x = formula.tensor((4, 3, 64, 25, 2), 45, 1.0).to(dev)
+    y = torch.tensor([5, 6, 7, 8], device=dev)
+    seen, grads = {}, {}
+    for mode in (0, 1):
+        old, oldb = fused.ASYNC_DW, fused.BATCH_SIDE
+        fused.ASYNC_DW = fused.BATCH_SIDE = mode
+        try:
+            m = _model(dev)
+            for name in ("l3.gcn1.Feature_Mask", "l6.tcn1.shift_in.ypos",
+                         "l2.gcn1.Feature_Mask"):
+                p = m.get_parameter(name)
+                p.register_post_accumulate_grad_hook(
+                    lambda t, k=(mode, name): seen.__setitem__(k, t.grad.detach().clone()))
+            for p in m.parameters():
+                p.grad = None
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            torch.cuda.synchronize()
+            grads[mode] = {n: p.grad.cpu() for n, p in m.named_parameters()
+                           if p.grad is not None}
+            for name in ("l3.gcn1.Feature_Mask", "l6.tcn1.shift_in.ypos",
+                         "l2.gcn1.Feature_Mask"):   # the hook saw the final .grad
+                assert torch.equal(seen[(mode, name)].cpu(), grads[mode][name]), name
+        finally:
+            fused.ASYNC_DW, fused.BATCH_SIDE = old, oldb
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+    assert float(grads[1]["l3.gcn1.Feature_Mask"].abs().max()) > 0
+
+
+def _twice_grads(dev, async_dw, one_graph, slots=False):
+    """Gradients of CE(m(a)) + CE(m(b)): summed in ONE backward (the model used twice in
+    one graph), or as two backward passes accumulating into .grad."""
+    from shiftgcn import fused
+    from shiftgcn.dist import GradAllReduce
+    old = fused.ASYNC_DW
+    fused.ASYNC_DW = async_dw
+    ga = None
+    try:
+        m = _model(dev)
+        if slots:   # gradient bucket slots registered (the data-parallel step)
+            ga = GradAllReduce(m)
+        a = formula.tensor((4, 3, 64, 25, 2), 46, 1.0).to(dev)
+        b = formula.tensor((4, 3, 64, 25, 2), 47, 1.0).to(dev)
+        ya = torch.tensor([1, 2, 3, 4], device=dev)
+        yb = torch.tensor([9, 8, 7, 6], device=dev)
+        for p in m.parameters():
+            p.grad = None
+        ce = torch.nn.functional.cross_entropy
+        if one_graph:
+            (ce(m(a), ya) + ce(m(b), yb)).backward()
+        else:
+            ce(m(a), ya).backward()
+            ce(m(b), yb).backward()
+        if ga is not None:
+            ga()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()
+                if p.grad is not None}
+    finally:
+        fused.ASYNC_DW = old
+        if ga is not None:
+            ga.close()
+
+
+def test_model_used_twice_in_one_graph():
+    """a parameter with two gradient contributions in one backward.
+    The deferred writes (side stream, end-of-backward finalizes) and the gradient bucket
+    slots must not hand autograd a tensor it sums before it is written, nor the same slot
+    twice: one backward over model(a) + model(b) equals two accumulating backward passes,
+    with and without the side stream and with the data-parallel bucket registered."""
+    import socket
+
+    import torch.distributed as dist
+    dev = torch.device("cuda:0")
+    ref = _twice_grads(dev, 0, one_graph=False)
+    for async_dw in (1, 0):
+        got = _twice_grads(dev, async_dw, one_graph=True)
+        assert got.keys() == ref.keys() and len(got) > 100
+        for n in ref:
+            torch.testing.assert_close(got[n], ref[n], rtol=1e-6, atol=1e-7, msg=n)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1)
+    try:
+        got = _twice_grads(dev, 1, one_graph=True, slots=True)
+        for n in ref:
+            torch.testing.assert_close(got[n], ref[n], rtol=1e-6, atol=1e-7, msg=n)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_autograd_grad_calls_get_distinct_slots():
+    """two torch.autograd.grad calls while the bucket is registered
+    return tensors that do not alias each other (a slot goes to one gradient per backward)."""
+    import shiftgcn
+    from shiftgcn import ops
+    dev = torch.device("cuda:0")
+    u = shiftgcn.TCN_GCN_unit(64, 64, None, num_point=25)
+    formula.fill_state(u, seed=8)
+    u = u.to(dev).train()
+    ps = [p for p in u.parameters() if p.requires_grad]
+    x1 = formula.tensor((2, 64, 16, 25), 50, 1.0).to(dev)
+    x2 = formula.tensor((2, 64, 16, 25), 51, 1.0).to(dev)
+    # references without a bucket (training-mode outputs use batch statistics, so the
+    # running-statistics updates between calls change nothing)
+    ref1 = [t.clone() for t in torch.autograd.grad(u(x1).square().sum(), ps)]
+    ref2 = [t.clone() for t in torch.autograd.grad(u(x2).square().sum(), ps)]
+    flat = torch.zeros(sum(p.numel() for p in ps), device=dev)
+    ops.register_grad_slots([(str(i), p) for i, p in enumerate(ps)], flat)
+    try:
+        g1 = torch.autograd.grad(u(x1).square().sum(), ps)
+        g2 = torch.autograd.grad(u(x2).square().sum(), ps)
+        torch.cuda.synchronize()
+        lo, hi = flat.data_ptr(), flat.data_ptr() + 4 * flat.numel()
+        assert all(lo <= a.data_ptr() < hi for a in g1)          # the first got the slots
+        assert not any(lo <= b.data_ptr() < hi for b in g2)      # the second fresh memory
+        for a, r in zip(g1, ref1):   # ... and did not overwrite the first one's results
+            assert torch.equal(a, r)
+        for b, r in zip(g2, ref2):
+            assert torch.equal(b, r)
+    finally:
+        ops.unregister_grad_slots(ps)
+        ops.release_grad_slots(ps)

@@ -1,6 +1,6 @@
 # Same-box A/B of env-knob settings of the in-tree library, interleaved REPS times:
 #   gpurun -- 'TAG=r04_ens BENCH_ARGS="--config ens" REPS=2 \
-#              SETS="old:SGCN_EVAL_GCN_EPI=0 epi: fused:SGCN_EVAL_TSHIFT_FUSION_MIN_C=0" \
+#              SETS="base: nofold:SGCN_EVAL_FOLD=0" \
 #              bash tools/gpu_envab.sh'
 # A set is name:VAR=V,VAR=V (empty after the colon = defaults).
 set -e
