@@ -1401,11 +1401,17 @@ int pick_lpt(int n, int nt) {
 }
 
 // elements per thread of the joint-aligned stride-1 LDS backward kernels (stride
-// (nt / W) * W); 0 = the plane does not fit 32 per thread
+// (nt / W) * W); 0 = the plane does not fit 32 per thread. 512-thread workgroups also take
+// 12 and 20: a thread holds ~5 VGPRs per element, and at 24 the shift_out backward (bnin)
+// and the GBD backward held 141-143 VGPRs — one 512-thread workgroup per CU on MediaPipe's
+// 9,900-float planes (W = 33, exactly 20 per thread); at 20 two fit (likewise 12 against 16
+// for its 4,950-float T = 150 planes: three instead of two)
 int ra_lpt(int n, int nt, int W) {
   const int nte = (nt / W) * W;
   if (nte <= 0 || W > 64) return 0;
   const int per = (n + nte - 1) / nte;
+  if (nt == 512 && per > 8 && per <= 12) return 12;
+  if (nt == 512 && per > 16 && per <= 20) return 20;
   return per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 24 ? 24 : (per <= 32 ? 32 : 0)));
 }
 
@@ -1414,6 +1420,9 @@ int ra_lpt(int n, int nt, int W) {
 // (7,500 floats) measured 8 % (GBN) / 4 % (plain) faster than 512 threads; the shift_out
 // backward (bnin) keeps 512 threads above 4,096 floats (no difference)
 constexpr int kRaSplit256 = 8192;
+#ifndef SGCN_GBD_SPLIT
+#define SGCN_GBD_SPLIT 1
+#endif
 
 // LDS bytes of the padded stride-1 backward (GBN reuses it for 6*NT partial sums)
 size_t ra_lds_bytes(int H, int W, int nt, bool gbn) {
@@ -1442,7 +1451,8 @@ bool launch_ra(int nt, const float* gout, const float* in, const float* xpos,
   if (nt == 256) {
     if (lpt == 8) SGCN_RA(256, 8); else if (lpt == 16) SGCN_RA(256, 16); else if (lpt == 24) SGCN_RA(256, 24); else SGCN_RA(256, 32);
   } else {
-    if (lpt == 8) SGCN_RA(512, 8); else if (lpt == 16) SGCN_RA(512, 16); else if (lpt == 24) SGCN_RA(512, 24); else SGCN_RA(512, 32);
+    if (lpt == 8) SGCN_RA(512, 8); else if (lpt == 12) SGCN_RA(512, 12); else if (lpt == 16) SGCN_RA(512, 16);
+    else if (lpt == 20) SGCN_RA(512, 20); else if (lpt == 24) SGCN_RA(512, 24); else SGCN_RA(512, 32);
   }
 #undef SGCN_RA
   return true;
@@ -1710,9 +1720,13 @@ int sgcn_tshift_bwd_gbn(const float* gout, const float* in, const float* xpos,
   float2* pg = (float2*)ws;
   float2* bp = (float2*)bn_part;
   // sgcn_tshift_bwd's stride-1 thread counts; elements per thread from the W-aligned
-  // stride (NT / W) * W; 512 threads when 256 would need more than 32 per thread
+  // stride (NT / W) * W; 512 threads when 256 would need more than 32 per thread. With the
+  // down BatchNorm's sums (GBD) a 32-element thread holds 183 VGPRs (two 256-thread
+  // workgroups per CU): such planes take 512 threads x 16 (107 VGPRs, two 512-thread
+  // workgroups) (SGCN_GBD_SPLIT=0: 256 threads as GBN)
   const int n = H * W;
-  const int ntg = n <= kRaSplit256 && ra_lpt(n, 256, W) ? 256 : kBwdThreads;
+  const int l256 = n <= kRaSplit256 ? ra_lpt(n, 256, W) : 0;
+  const int ntg = l256 && !(SGCN_GBD_SPLIT && d && l256 > 24) ? 256 : kBwdThreads;
   const bool ok =
       d ? launch_ra<true, false, true, false, true, true>(
               ntg, gout, in, xpos, ypos, in_scale, in_shift, bn_mean, bn_invstd, gin, pg, bp, B,

@@ -142,12 +142,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_gradients_are_written_into_the_bucket():
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_gradients_are_written_into_the_bucket(backend):
     """Config 5's N>1 step (verdict r03): the HIP backward writes every trainable gradient
     straight into GradAllReduce's flat bucket, so the call copies nothing (one all-reduce,
-    then the deferred 1/world inside the one-launch optimizer update). A world-1 gloo group
-    on the GPU: every scale is 1 and the step must be bit-identical to the same step with no
-    process group (no bucket, no slots)."""
+    then the deferred 1/world inside the one-launch optimizer update). A world-1 group on the
+    GPU — gloo, and RCCL (torch's "nccl" backend: the collective bench.py uses at N > 1, here
+    with its one rank): every scale is 1 and the step must be bit-identical to the same step
+    with no process group (no bucket, no slots)."""
     import torch.distributed as dist
     import shiftgcn  # noqa: F401
     from shiftgcn import train
@@ -159,9 +161,11 @@ def test_gradients_are_written_into_the_bucket():
     o_ref = train.build_optimizer(m_ref, base_lr=0.1)
     for _ in range(2):
         train.train_step(m_ref, o_ref, x, labels)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
-                            world_size=1)
+    kw = {"device_id": torch.device(DEV, 0)} if backend == "nccl" else {}
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, **kw)
     try:
+        assert dist.get_backend() == backend
         m = _ours()
         opt = train.build_optimizer(m, base_lr=0.1)
         assert isinstance(opt, train.FusedSGD)
