@@ -235,11 +235,16 @@ __global__ void tshift_params_kernel(const float* __restrict__ xpos,
 // from per-element selects. Only the joint-shift rotation (XROT) and the feature mask
 // cost VALU per loaded element.
 // ------------------------------------------------------------------------------------
+//
+// AR (K <= 64, the HBM-bound 64-row tiles): the whole A (K x BM) is staged into LDS once in
+// the prologue and B is single-buffered (a second barrier per stage): 35 instead of 43 KB of
+// LDS, so four workgroups fit a CU instead of three — a third more operand bytes in flight.
 template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM,
-          bool TSH = false>
+          bool TSH = false, bool AR = false>
 __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   SGCN_CRIT_PRIO();
   static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
+  static_assert(!AR || !TSH, "AR: plain contraction");
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = 16;
   constexpr int MI = BM / WM / 32;
@@ -251,9 +256,12 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   static_assert(MI >= 1 && NJ >= 1 && A_PER >= 1 && B_PER >= 1, "bad tile");
   static_assert((BM * BK) % NT == 0 && NT % BN == 0 && NT % BK == 0 && NT % BM == 0, "bad tile");
   // operand stages; the epilogue reuses the same memory to stage the accumulator tile
-  __shared__ float smem[2 * BK * AP + 2 * BK * BP];
+  constexpr int KAR = 64;                          // AR: the largest K held resident
+  constexpr int ASZ = AR ? KAR * AP : 2 * BK * AP;
+  constexpr int BSZ = AR ? BK * BP : 2 * BK * BP;
+  __shared__ float smem[ASZ + BSZ];
   float (*As)[BK * AP] = reinterpret_cast<float (*)[BK * AP]>(smem);
-  float (*Bs)[BK * BP] = reinterpret_cast<float (*)[BK * BP]>(smem + 2 * BK * AP);
+  float (*Bs)[BK * BP] = reinterpret_cast<float (*)[BK * BP]>(smem + ASZ);
   __shared__ float bias_s[BM];
   __shared__ int rot_s[BM];
   __shared__ unsigned ycol_s[BN];   // per tile column: byte offset of (b, t) in Y
@@ -356,6 +364,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         cv = cv >= V ? cv - V : cv;
       }
     }
+    if (AR) return;   // A is resident (staged in the prologue)
     const unsigned ak0 = AMC ? (unsigned)(k0 * lda * 4) : (unsigned)(k0 * 4);
 #pragma unroll
     for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i)
@@ -381,8 +390,9 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         // is formed exactly once when one M-block covers all M)
         if (p.xs) bstore(xsr, val, colok ? xcol : p.x_bytes, (unsigned)row * xcs4);
       }
-      Bs[buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
+      Bs[AR ? 0 : buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
     }
+    if (AR) return;
 #pragma unroll
     for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i) {
       const int m = AMC ? am : am + i * (NT / BK);
@@ -399,6 +409,30 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
 
   const int kl = lane >> 5, cl = lane & 31;
   const int nstage = (K + BK - 1) / BK;
+  if constexpr (AR) {
+    // the whole A (K <= 64 rows of BM) into LDS at row k, every stage's loads in flight at
+    // once (rows past K: out of range, 0)
+    float raa[KAR / BK][A_PER];
+#pragma unroll
+    for (int st = 0; st < KAR / BK; ++st) {
+      const int k0 = st * BK;
+      const unsigned ak0 = AMC ? (unsigned)(k0 * lda * 4) : (unsigned)(k0 * 4);
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        const bool in = k0 + (AMC ? ak + i * (NT / BM) : ak) < K;
+        raa[st][i] = bload(ar, in ? (AMC ? avoff : (k0 < kspan ? avoff : p.a_bytes)) : p.a_bytes,
+                           ak0 + (unsigned)i * astep);
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < KAR / BK; ++st)
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        const int m = AMC ? am : am + i * (NT / BK);
+        const int k = AMC ? ak + i * (NT / BM) : ak;
+        smem[(st * BK + k) * AP + m] = raa[st][i];
+      }
+  }
   load_stage(0);
   store_stage(0, 0);
   __syncthreads();
@@ -412,8 +446,9 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
       }
       load_stage((s + 1) * BK);
     }
-    const float* __restrict__ Aw = As[cur] + kl * AP + wm * (BM / WM) + cl;
-    const float* __restrict__ Bw = Bs[cur] + kl * BP + wn * (BN / WN) + cl;
+    const float* __restrict__ Aw = (AR ? smem + s * BK * AP : As[cur]) + kl * AP +
+                                   wm * (BM / WM) + cl;
+    const float* __restrict__ Bw = Bs[AR ? 0 : cur] + kl * BP + wn * (BN / WN) + cl;
     float af[2][MI], bf[2][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i) af[0][i] = Aw[i * 32];
@@ -436,7 +471,10 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[c2][i], bf[c2][j], acc[i][j],
                                                            0, 0, 0);
     }
-    if (s + 1 < nstage) store_stage(cur ^ 1, (s + 1) * BK);
+    if (s + 1 < nstage) {
+      if (AR) __syncthreads();   // single B buffer: every wave has read this stage
+      store_stage(cur ^ 1, (s + 1) * BK);
+    }
     __syncthreads();
   }
 
@@ -453,7 +491,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   constexpr int NW = WM * WN;
   constexpr int RB = WM * 16;      // staged rows per pass
   constexpr int CQ = BN / 64;      // 64-column groups per row
-  static_assert(BN % 64 == 0 && RB * BN <= 2 * BK * (AP + BP), "epilogue staging");
+  static_assert(BN % 64 == 0 && RB * BN <= ASZ + BSZ, "epilogue staging");
   unsigned ycolq[CQ];
   int vq[CQ];
 #pragma unroll
@@ -1162,13 +1200,13 @@ __global__ __launch_bounds__(256) void pw_fwd_smallm_kernel(FwdArgs p) {
 // ------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool AR = false>
 void launch_pwg(const FwdArgs& a, bool accum, hipStream_t st) {
   const long long P = (long long)a.B * a.T * a.V;   // < 2^31 (checked by the caller)
   dim3 grid((unsigned)((P + BN - 1) / BN), (a.M + BM - 1) / BM);
   const bool mask = a.mask != nullptr, xrot = a.x.rsign != 0, amc = a.a_mcontig != 0;
 #define SGCN_PWG(MS, XR, AM, AC) \
-  pwg_fwd_kernel<BM, BN, WM, WN, MS, XR, AM, AC><<<grid, 64 * WM * WN, 0, st>>>(a)
+  pwg_fwd_kernel<BM, BN, WM, WN, MS, XR, AM, AC, false, AR><<<grid, 64 * WM * WN, 0, st>>>(a)
 #define SGCN_PWG_AC(MS, XR, AM) \
   (accum ? SGCN_PWG(MS, XR, AM, true) : SGCN_PWG(MS, XR, AM, false))
 #define SGCN_PWG_AM(MS, XR) (amc ? SGCN_PWG_AC(MS, XR, true) : SGCN_PWG_AC(MS, XR, false))
@@ -1289,6 +1327,9 @@ int dw_tile(int X) { return X > 64 ? 128 : 64; }
 #define SGCN_SMALLM 1
 #endif
 bool use_dwc(int Nc) { return SGCN_DWC && Nc <= kDwcMaxC; }
+#ifndef SGCN_PW_AR
+#define SGCN_PW_AR 1   // A/B knob: the A-resident K <= 64 forward tile (pwg_fwd_kernel AR)
+#endif
 int dwc_splits(int M, long long P) {
   const int mg = (M + 4 * kDwcRows - 1) / (4 * kDwcRows);
   long long S = (1024 + mg - 1) / mg;
@@ -1372,7 +1413,12 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
       if (ac) pw_fwd_smallm_kernel<false, true><<<grid, 256, 0, st>>>(a);
       else pw_fwd_smallm_kernel<false, false><<<grid, 256, 0, st>>>(a);
     }
-  } else if (M <= 64) launch_pwg<64, 256, 2, 4>(a, ac, st);
+  } else if (M <= 64) {
+    // 16 < K <= 64 (HBM-bound): A resident in LDS, one B buffer -> four workgroups per CU
+    // (one K stage, K <= 16, gains nothing from it: l1's K = 3 measured 4 % slower)
+    if (K > 16 && K <= 64 && SGCN_PW_AR) launch_pwg<64, 256, 2, 4, true>(a, ac, st);
+    else launch_pwg<64, 256, 2, 4>(a, ac, st);
+  }
   // 64 < M <= 128: 128 x 128 tiles on 8 waves (32 x 64 per wave, twice the workgroups of
   // the 128 x 256 tile): pw_fwd class -1.8 %, step +0.1..0.25 % same-box
   // (profiles/r04_tiles/; 64 x 128 / 4-wave tiles at M <= 64 and 128 x 128 / 256 x 64

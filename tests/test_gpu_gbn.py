@@ -161,7 +161,14 @@ def test_gbn_down_sums_match_two_pass(case):
     dA2, gx2, gy2, part2, z6d, d6 = ops.tshift_bwd_gbn(dAs, H, xpos, ypos, ast, Z, zst,
                                                         down=(D, dst))
     torch.cuda.synchronize()
-    assert torch.equal(dA1, dA2) and torch.equal(part1, part2) and torch.equal(z6, z6d)
+    assert torch.equal(dA1, dA2)
+    if -(-T * V // ((256 // V) * V)) <= 24:   # the same 256-thread launch for both forms
+        assert torch.equal(part1, part2) and torch.equal(z6, z6d)
+    else:
+        # planes that need 32 elements per thread on 256 threads run the GBD form on 512
+        # threads x 16 (register pressure, tshift.hip SGCN_GBD_SPLIT): the same plane sums,
+        # added in another order
+        assert _rel(part2, part1) < 1e-6 and _rel(z6d, z6) < 1e-6
     coefA, _, _ = ops.bn_bwd_finalize(part1, B, C, B * T * V, ast, bn_t)
     rp, rpart = ops.bn_bwd_reduce(dA1, H, True, Z, zst, 3, r=D, rst=dst, dy_coef=coefA)
     c_ref, dg_ref, db_ref = ops.bn_bwd_finalize(rpart, B, C, B * T * V, dst, bn_d)

@@ -178,6 +178,7 @@ int main(int argc, char** argv) {
       if (msk) dw_s<64, 64, 2, 2, true, false>(c, d, S0 * f, tag);
       else dw_s<64, 64, 2, 2, false, true>(c, d, S0 * f, tag);
     }
+    if (!msk) dw_s<64, 64, 2, 2, false, true>(c, d, S0, "product again");   // warm state
     for (int tg : {1024, 2048, 4096}) {
       char tag[64];
       snprintf(tag, sizeof tag, "dw3 bkp16 t%d", tg);
