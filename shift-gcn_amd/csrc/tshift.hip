@@ -1310,7 +1310,11 @@ void launch_fwd_lds(bool affine, bool stats, const float* in, float* out, const 
 int pad_fwd_lpt(int H, int W, int nt) {
   if (W > 64) return 0;
   const int ntj = (nt / W) * W, per = (H * W + ntj - 1) / ntj;
-  const int lpt = per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 24 ? 24 : (per <= 32 ? 32 : 0)));
+  // 512 threads also at 12 / 20 (as ra_lpt): MediaPipe's 9,900-float planes are 20 per
+  // thread, and the eval pre / tail forms held 88-95 VGPRs at 24 (two workgroups per CU)
+  int lpt = per <= 8 ? 8 : (per <= 16 ? 16 : (per <= 24 ? 24 : (per <= 32 ? 32 : 0)));
+  if (nt == 512 && per > 8 && per <= 12) lpt = 12;
+  if (nt == 512 && per > 16 && per <= 20) lpt = 20;
   return (size_t)(ra_pad_floats(H, W) + 1) * sizeof(float) > 65536 ? 0 : lpt;
 }
 
@@ -1334,7 +1338,8 @@ bool launch_fwd_pad(bool affine, bool stats, const float* in, float* out, const 
     if (affine) { if (stats) SGCN_FWDP(L, true, true); else SGCN_FWDP(L, true, false); }     \
     else { if (stats) SGCN_FWDP(L, false, true); else SGCN_FWDP(L, false, false); }          \
   } while (0)
-  if (lpt == 8) SGCN_FWDP_AS(8); else if (lpt == 16) SGCN_FWDP_AS(16); else if (lpt == 24) SGCN_FWDP_AS(24); else SGCN_FWDP_AS(32);
+  if (lpt == 8) SGCN_FWDP_AS(8); else if (lpt == 12) SGCN_FWDP_AS(12); else if (lpt == 16) SGCN_FWDP_AS(16);
+  else if (lpt == 20) SGCN_FWDP_AS(20); else if (lpt == 24) SGCN_FWDP_AS(24); else SGCN_FWDP_AS(32);
 #undef SGCN_FWDP_AS
 #undef SGCN_FWDP
   return true;
@@ -1543,7 +1548,8 @@ int sgcn_tshift_fwd_pre(const float* z, float* out, const float* xpos, const flo
       if (nt == kThreads) {
         if (lpt == 8) SGCN_PREP_R(kThreads, 8); else if (lpt == 16) SGCN_PREP_R(kThreads, 16); else if (lpt == 24) SGCN_PREP_R(kThreads, 24); else SGCN_PREP_R(kThreads, 32);
       } else {
-        if (lpt == 8) SGCN_PREP_R(512, 8); else if (lpt == 16) SGCN_PREP_R(512, 16); else if (lpt == 24) SGCN_PREP_R(512, 24); else SGCN_PREP_R(512, 32);
+        if (lpt == 8) SGCN_PREP_R(512, 8); else if (lpt == 12) SGCN_PREP_R(512, 12); else if (lpt == 16) SGCN_PREP_R(512, 16);
+        else if (lpt == 20) SGCN_PREP_R(512, 20); else if (lpt == 24) SGCN_PREP_R(512, 24); else SGCN_PREP_R(512, 32);
       }
 #undef SGCN_PREP_R
 #undef SGCN_PREP
@@ -1609,7 +1615,8 @@ int sgcn_tshift_fwd_tail(const float* in, float* out, const float* xpos, const f
       if (nt == kThreads) {
         if (lpt == 8) SGCN_TAILP_RG(kThreads, 8); else if (lpt == 16) SGCN_TAILP_RG(kThreads, 16); else if (lpt == 24) SGCN_TAILP_RG(kThreads, 24); else SGCN_TAILP_RG(kThreads, 32);
       } else {
-        if (lpt == 8) SGCN_TAILP_RG(512, 8); else if (lpt == 16) SGCN_TAILP_RG(512, 16); else if (lpt == 24) SGCN_TAILP_RG(512, 24); else SGCN_TAILP_RG(512, 32);
+        if (lpt == 8) SGCN_TAILP_RG(512, 8); else if (lpt == 12) SGCN_TAILP_RG(512, 12); else if (lpt == 16) SGCN_TAILP_RG(512, 16);
+        else if (lpt == 20) SGCN_TAILP_RG(512, 20); else if (lpt == 24) SGCN_TAILP_RG(512, 24); else SGCN_TAILP_RG(512, 32);
       }
 #undef SGCN_TAILP_RG
 #undef SGCN_TAILP
