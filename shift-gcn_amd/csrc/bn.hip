@@ -1157,9 +1157,6 @@ using namespace sgcn;
 // (7,500 floats) 256 x 30 measured 0.8 % faster per step than 512 x 15 (same box,
 // profiles/r03_bnja/ab_moments_reduce_t256.txt)
 constexpr int kJaSplit = 8192;
-#ifndef SGCN_DXF_SPLIT
-#define SGCN_DXF_SPLIT 1
-#endif
 
 // elements per thread of the plane-resident joint-aligned kernels on nt threads; 0 = the
 // plane does not fit (V > 64 or more than 32 per thread): the looping kernels take it
@@ -1560,11 +1557,9 @@ int sgcn_gcn_dx_finish(const float* dxt, const float* x0, const float* m, const 
   float2* pp = (float2*)prev_part;
   if (add2_mask) SGCN_REQUIRE(add1);
   {   // plane-resident joint-aligned kernel: V <= 64, <= 32 elements per thread
-    // (the identity-unit form, add2_mask, holds ~200 VGPRs at 32 elements per thread: two
-    // 256-thread workgroups per CU; above 4,096-float planes it takes 512 threads x 16,
-    // ~105 VGPRs and twice the waves (SGCN_DXF_SPLIT=0: 256 threads up to kJaSplit))
-    const int split = add2_mask && SGCN_DXF_SPLIT ? 4096 : kJaSplit;
-    const int nt = T * V <= split ? kThreads : 512;
+    // (the identity-unit form holds ~200 VGPRs at 256 x 32 — two workgroups per CU — but
+    // 512 x 16, twice the waves, measured 2 % slower: profiles/r05_ar/ab_dx_finish_512.txt)
+    const int nt = T * V <= kJaSplit ? kThreads : 512;
     const int lpt = ja_lpt(T, V, nt);
     if (lpt) {
 #define SGCN_FJ(NT, L, A1, A2, PT, AM)                                                         \
