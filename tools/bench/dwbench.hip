@@ -137,6 +137,47 @@ void big(hipStream_t st, float* x, float* y, float* mask, float* ws, float* dw1,
   }
 }
 
+// the 256-row weight gradients (l9 / l10 at T = 75: 256 x 256; l8's gcn at T = 150: 256 x 128):
+// the split count sets the slab traffic (S x M x Nc floats written, then read by the reduce)
+void huge(hipStream_t st, float* x, float* y, float* ws, float* dw1, float* dw2) {
+  const int B = 128, V = 25;
+  struct S3 { int M, K, T; };
+  for (S3 sh : {S3{256, 256, 75}, S3{256, 128, 150}}) {
+    const int M = sh.M, K = sh.K, T = sh.T, N = T * V;
+    DwArgs d{};
+    d.g = {y, (long long)M * N, N, 1, 0};
+    d.x = {x, (long long)K * N, N, 1, 0};
+    d.M = M; d.Nc = K; d.T = T; d.V = V; d.B = B;
+    d.g_bytes = plane_bytes(d.g.bstride, d.g.cstride, 1, B, M, T, V);
+    d.x_bytes = plane_bytes(d.x.bstride, d.x.cstride, 1, B, K, T, V);
+    const double by = 4.0 * B * N * (M + K), fl = 2.0 * B * N * M * K;
+    char name[32];
+    snprintf(name, sizeof name, "%dx%d T%d", M, K, T);
+    Ctx c{st, ws, nullptr, dw1, by, name, fl};
+    {
+      DwArgs a = d;
+      const int S = launch_dw3(a, st, ws, false);
+      auto L = [&]() {
+        launch_dw3(a, st, ws, false);
+        launch_slab_reduce(ws, nullptr, S, M, K, dw1, 0, 0, nullptr, 0, st);
+      };
+      for (int r = 0; r < 2; ++r) {
+        const float u = timeit(L, st, 20);
+        printf("%-18s %-22s S=%5d %7.1f us (with reduce) %.3f of 157.3 TF\n", name, "product",
+               S, u, fl / u / 1e6 / 157.3);
+      }
+    }
+    c.dwref = dw1;
+    c.dwout = dw2;
+    for (int tg : {256, 384, 512, 768, 1024}) {
+      char tag[64];
+      snprintf(tag, sizeof tag, "target %d", tg);
+      if (K == 256) dw3_t<16, false, false, 256, 256, 4, 2>(c, d, tg, tag);
+      else dw3_t<16, false, false, 256, 128, 4, 2>(c, d, tg, tag);
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const int B = 128, M = 64, K = 64, T = 300, V = 25;
   const int N = T * V;
@@ -151,6 +192,11 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(y, h.data() + 7, (ne - 7) * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(mask, h.data(), V * K * 4, hipMemcpyHostToDevice));
   const double by = 4.0 * B * N * (M + K);
+  if (argc > 1 && argv[1][0] == 'h') {
+    huge(st, x, y, ws, dw1, dw2);
+    printf("done\n");
+    return 0;
+  }
   if (argc > 1 && argv[1][0] == 'b') {
     big(st, x, y, mask, ws, dw1, dw2);
     printf("done\n");
