@@ -70,15 +70,16 @@ void dw_variant(const char* name, const Shape& s, DwArgs a, int S, hipStream_t s
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool AR = false>
 void fwd_variant(const Shape& s, const FwdArgs& a, hipStream_t st, const float* yref,
                  double fl, double by) {
-  if (a.M > BM) return;
-  auto L = [&]() { launch_pwg<BM, BN, WM, WN>(a, false, st); };
+  if (a.M > BM || (AR && a.K > 64)) return;
+  auto L = [&]() { launch_pwg<BM, BN, WM, WN, AR>(a, false, st); };
   float us = timeit(L, st, 20);
   const size_t n = (size_t)s.B * s.M * s.T * s.V;
-  printf("%-20s fwd %3dx%3d w%dx%d            %8.1f us  %6.1f TF/s  %6.2f TB/s  %s\n", s.name,
-         BM, BN, WM, WN, us, fl / us / 1e6, by / us / 1e6, same(yref, a.y.ptr, n) ? "bit-exact" : "MISMATCH");
+  printf("%-20s fwd %3dx%3d w%dx%d%s         %8.1f us  %6.1f TF/s  %6.2f TB/s  %s\n", s.name,
+         BM, BN, WM, WN, AR ? " AR" : "   ", us, fl / us / 1e6, by / us / 1e6,
+         same(yref, a.y.ptr, n) ? "bit-exact" : "MISMATCH");
 }
 
 int main(int argc, char** argv) {
@@ -147,6 +148,11 @@ int main(int argc, char** argv) {
         v.a_bytes = (unsigned)(s.M * s.K * 4);
         v.mask_bytes = s.mask ? (unsigned)(s.V * s.K * 4) : 0u;
         fwd_variant<64, 256, 2, 4>(s, v, st, y2, fl, by);
+        fwd_variant<64, 256, 2, 4, true>(s, v, st, y2, fl, by);
+        fwd_variant<64, 128, 1, 4, true>(s, v, st, y2, fl, by);
+        fwd_variant<64, 128, 2, 2, true>(s, v, st, y2, fl, by);
+        fwd_variant<64, 256, 2, 4>(s, v, st, y2, fl, by);
+        fwd_variant<64, 256, 2, 4, true>(s, v, st, y2, fl, by);
         fwd_variant<64, 128, 1, 4>(s, v, st, y2, fl, by);
         fwd_variant<64, 512, 2, 4>(s, v, st, y2, fl, by);
         fwd_variant<64, 256, 1, 4>(s, v, st, y2, fl, by);
