@@ -85,6 +85,34 @@ void fwd_variant(const Shape& s, const FwdArgs& a, hipStream_t st, const float* 
 int main(int argc, char** argv) {
   const bool do_fwd = argc < 2 || strchr(argv[1], 'f');
   const bool do_dw = argc < 2 || strchr(argv[1], 'w');
+  if (argc > 1 && strchr(argv[1], 'q')) {
+    // tile quantization: the product forward at batch sizes around the model's, time per
+    // 128-/256-position tile (tiles = P / BN; workgroup slots: 512 at M = 256, 768 at
+    // M = 128, 1024 at M <= 64 with K <= 64)
+    hipStream_t st; CK(hipStreamCreate(&st));
+    const size_t maxe = (size_t)160 * 256 * 75 * 25 * 2;
+    float *x, *y, *w;
+    CK(hipMalloc(&x, maxe * 4)); CK(hipMalloc(&y, maxe * 4)); CK(hipMalloc(&w, 256 * 256 * 4));
+    CK(hipMemset(x, 0, maxe * 4)); CK(hipMemset(w, 0, 256 * 256 * 4));
+    struct Q { const char* name; int M, K, T, bn; };
+    Q qs[] = {{"l9 tcn 256 T75", 256, 256, 75, 128}, {"l6 tcn 128 T150", 128, 128, 150, 128},
+              {"l2 tcn 64 T300", 64, 64, 300, 256}};
+    for (int rep = 0; rep < 2; ++rep)
+      for (auto& q : qs)
+        for (int B : {112, 120, 128, 132, 136, 140, 144, 150}) {
+          const long long N = (long long)q.T * 25;
+          if ((size_t)B * q.K * N > maxe || (size_t)B * q.M * N > maxe) continue;
+          auto L = [&]() {
+            sgcn_pw_fwd(w, 0, nullptr, x, q.K * N, N, 1, 0, nullptr, y, q.M * N, N, 1, 0, 0, 0,
+                        B, q.M, q.K, q.T, 25, st);
+          };
+          const float us = timeit(L, st, 20);
+          const double tiles = (double)B * N / q.bn;
+          printf("%-18s B=%3d tiles %6.0f  %8.1f us  %6.4f us/tile  %6.1f TF/s\n", q.name, B, tiles,
+                 us, us / tiles, 2.0 * B * N * q.M * q.K / us / 1e6);
+        }
+    return 0;
+  }
   Shape shapes[] = {
     {"l2 tcn 64x64 T300", 128, 64, 64, 300, 25, false, false},
     {"l2 gcn 64x64 T300", 128, 64, 64, 300, 25, true, true},
