@@ -63,7 +63,7 @@ __device__ __forceinline__ unsigned rowb(const Args& a, int r) {
 
 // (1) register loads, 16-row stages double-buffered in registers, plain stores (the
 // product's memory pattern without the MFMA): each lane one column, W floats per access
-template <int W, int BN>
+template <int W, int BN, int POL = 0>
 __global__ __launch_bounds__(512) void reg_copy(Args a) {
   const int tid = threadIdx.x;
   constexpr int LPR = BN / W;            // lanes per row
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(512) void reg_copy(Args a) {
         v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, col, rowb(a, r0 + i * RPI), 0));
 #pragma unroll
       for (int i = 0; i < 64 / RPI; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v[i]) , yr, col, rowb(a, r0 + i * RPI), 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v[i]) , yr, col, rowb(a, r0 + i * RPI), POL);
     } else {
       float v[64 / RPI];
 #pragma unroll
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(512) void reg_copy(Args a) {
         v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col, rowb(a, r0 + i * RPI), 0));
 #pragma unroll
       for (int i = 0; i < 64 / RPI; ++i)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), yr, col, rowb(a, r0 + i * RPI), 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), yr, col, rowb(a, r0 + i * RPI), POL);
     }
   }
 }
@@ -178,6 +178,29 @@ __global__ __launch_bounds__(512) void tile_read(Args a) {
   if (acc == 1.2345f) a.y[0] = acc;
 }
 
+// (4) flat copies with more in flight: U float4 per thread per iteration (all loads, then
+// all stores), optionally non-temporal stores
+template <int U, bool NT>
+__global__ __launch_bounds__(512) void flat_copy_u(const f32x4* __restrict__ x, f32x4* __restrict__ y, size_t n4) {
+  const size_t stride = (size_t)gridDim.x * 512 * U;
+  for (size_t i0 = blockIdx.x * 512ull * U + threadIdx.x; i0 < n4; i0 += stride) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = i0 + u * 512 < n4 ? x[i0 + u * 512] : f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * 512 < n4) {
+        if (NT) __builtin_nontemporal_store(v[u], &y[i0 + u * 512]);
+        else y[i0 + u * 512] = v[u];
+      }
+  }
+}
+// (5) write-only stream (float4)
+__global__ __launch_bounds__(512) void flat_fill(f32x4* __restrict__ y, size_t n4) {
+  for (size_t i = blockIdx.x * 512ull + threadIdx.x; i < n4; i += (size_t)gridDim.x * 512)
+    y[i] = f32x4{1.f, 2.f, 3.f, 4.f};
+}
+
 template <typename F>
 float timeit(F&& launch, int reps) {
   hipEvent_t e0, e1;
@@ -206,7 +229,7 @@ int main() {
     const bool ok = memcmp(g.data(), h.data(), n * 4) == 0;
     printf("%-34s %8.1f us  %6.2f TB/s  %s\n", nm, us, by / us / 1e6, ok ? "ok" : "WRONG");
   };
-  for (int rep = 0; rep < 4; ++rep) {
+  for (int rep = 0; rep < 2; ++rep) {
     const int NL = rep & 1 ? 7500 : 0;
     printf("layout: %s\n", NL ? "model planes (b, c, t, v), N = 7500" : "rows of 960k positions");
 #define RUN(NM, K, BN, G)                                                                    \
@@ -222,6 +245,23 @@ int main() {
       report("flat float4 copy g2048", us);
       us = timeit([&]() { flat_read<<<2048, 512>>>((const f32x4*)x, y, n / 4); }, 20);
       printf("%-34s %8.1f us  %6.2f TB/s  (read only)\n", "flat float4 read g2048", us, n * 4.0 / us / 1e6);
+      us = timeit([&]() { flat_fill<<<2048, 512>>>((f32x4*)y, n / 4); }, 20);
+      printf("%-34s %8.1f us  %6.2f TB/s  (write only)\n", "flat float4 fill g2048", us, n * 4.0 / us / 1e6);
+      for (int gsz : {1024, 2048, 4096, 8192}) {
+        char nm[64];
+        CK(hipMemset(y, 0, n * 4));
+        us = timeit([&]() { flat_copy_u<4, false><<<gsz, 512>>>((const f32x4*)x, (f32x4*)y, n / 4); }, 20);
+        snprintf(nm, 64, "flat copy x4 g%d", gsz);
+        report(nm, us);
+        CK(hipMemset(y, 0, n * 4));
+        us = timeit([&]() { flat_copy_u<4, true><<<gsz, 512>>>((const f32x4*)x, (f32x4*)y, n / 4); }, 20);
+        snprintf(nm, 64, "flat copy x4 nt g%d", gsz);
+        report(nm, us);
+        CK(hipMemset(y, 0, n * 4));
+        us = timeit([&]() { flat_copy_u<1, false><<<gsz, 512>>>((const f32x4*)x, (f32x4*)y, n / 4); }, 20);
+        snprintf(nm, 64, "flat copy x1 g%d", gsz);
+        report(nm, us);
+      }
     }
     {
       Args a{x, y, P, P / 256, NL};
@@ -231,6 +271,9 @@ int main() {
       printf("%-34s %8.1f us  %6.2f TB/s  (read only)\n", "tile read dword BN256 g1024", us, n * 4.0 / us / 1e6);
     }
     RUN("reg dword BN256 g1024", (reg_copy<1, 256>), 256, 1024);
+    RUN("reg dword nt BN256 g1024", (reg_copy<1, 256, 2>), 256, 1024);
+    RUN("reg dword nt BN256 g2048", (reg_copy<1, 256, 2>), 256, 2048);
+    RUN("reg dwordx4 nt BN256 g2048", (reg_copy<4, 256, 2>), 256, 2048);
     RUN("reg dword BN256 g2048", (reg_copy<1, 256>), 256, 2048);
     RUN("reg dwordx4 BN256 g1024", (reg_copy<4, 256>), 256, 1024);
     RUN("reg dwordx4 BN256 g2048", (reg_copy<4, 256>), 256, 2048);
