@@ -76,6 +76,21 @@ __global__ __launch_bounds__(512) void k(const float* src, float* dst, float* ou
       for (int u = 0; u < 16; ++u) acc ^= v[u];   // one VALU per 256-B load
     }
     if (acc == 0x12345678u) out[0] = 1.f;
+  } else if (kind == 5) {
+    // register reads, 16 B per lane (buffer_load_dwordx4): a quarter of kind 1's instructions
+    // for the same bytes
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, -1, 0x00020000);
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    u4 acc = {0, 0, 0, 0};
+    for (unsigned i = 0; i < n; i += 16) {
+      u4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)lane * 16u, base + (i + 4 * u) * 256u, 0));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc ^= v[u];
+    }
+    if (acc.x == 0x12345678u) out[0] = 1.f;
   } else if (kind == 3 || kind == 4) {   // per 16-step: 16 (b32) / 4 (b128) instructions
     // LDS -> VGPR reads (ds_read_b32 / ds_read_b128), as many instructions as kind 1's loads
     // x 4 (b32) or x 1 (b128); values kept live by an empty asm (no VALU)
@@ -118,9 +133,10 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  const char* kn[] = {"LDS-DMA reads", "register reads", "stores", "ds_read_b32", "ds_read_b128"};
+  const char* kn[] = {"LDS-DMA reads", "register reads", "stores", "ds_read_b32", "ds_read_b128",
+                      "reg reads x4"};
   for (int rep = 0; rep < 2; ++rep)
-    for (int kind : {1, 3, 4})
+    for (int kind : {1, 5})
       for (int iters : {1500, 3000})
         for (int mode = 0; mode < 3; ++mode) {
           if (mode == 1 && iters != 1500) continue;
