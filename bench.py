@@ -428,6 +428,9 @@ def main():
                                             / n_meas / step_ms_meas, 4),
                 "whole_step_frac_of_fp32_peak": round(
                     value / world * GFLOP_PER_CLIP[args.config] / 1e3 / PEAK_FP32_TFLOPS, 4),
+                # context for the HBM-bound classes: what a plain copy of one activation
+                # (read + write, plain stores) reaches on this box in this run
+                "hbm_copy_gbs_measured": _copy_rate_gbs(dev, 4 * args.batch * M * 64 * T * V),
                 "schedule": ("timed steps: weight gradients on a side stream"
                              if async_dw else "timed steps: serialized") +
                             "; roofline/breakdown steps: serialized (each class timed alone)"}
@@ -466,6 +469,25 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _copy_rate_gbs(dev, nbytes, reps=10):
+    """Algorithmic GB/s of torch's copy_ of an nbytes fp32 tensor (read + write), event-timed:
+    the box's achievable rate for a one-read-one-write stream (tools/bench/streambench.hip
+    measures the hand-written forms: 5.0-5.8 TB/s, profiles/r05_dma/)."""
+    x = torch.ones(nbytes // 4, device=dev)
+    y = torch.empty_like(x)
+    y.copy_(x)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del x, y
+    return round(2 * nbytes / ms / 1e6, 1)
 
 
 def _max_over_ranks(elapsed, dev, world, steps):
