@@ -55,6 +55,7 @@ class FusedSGD(torch.optim.SGD):
                          weight_decay=weight_decay, nesterov=nesterov, foreach=True, **kw)
         self._layout = None   # (param signature, device numel / chunk map, n chunks)
         self._gscale = {}     # id(param) -> (param, gradient scale) for the next step only
+        self._cap = None      # (pinned table buffer, device table) for a step under capture
 
     def defer_grad_scale(self, pairs):
         """[(param, s)]: the next ``step`` first scales these parameters' gradients by s
@@ -139,7 +140,21 @@ class FusedSGD(torch.optim.SGD):
                     flags |= 2 | (bits << 32)
                     flags = struct.unpack("<q", struct.pack("<Q", flags))[0]
                 rows += [p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), wdlr, flags]
-        table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+        if torch.cuda.is_current_stream_capturing():
+            # hipGraph capture (bench.py --graph): no host allocation is allowed here, so the
+            # table goes through a pinned buffer and device table set up by an eager step;
+            # the captured copy re-reads the buffer at every replay (same addresses: the
+            # graph's gradients and buffers are static)
+            if self._cap is None or self._cap[0].numel() != len(rows):
+                raise RuntimeError("FusedSGD: run one eager step before capturing a graph")
+            host, table = self._cap
+            host.numpy()[:] = rows
+            table.copy_(host, non_blocking=True)
+        else:
+            table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+            if self._cap is None or self._cap[0].numel() != len(rows):
+                self._cap = (torch.empty(len(rows), dtype=torch.int64).pin_memory(),
+                             torch.empty(len(rows), dtype=torch.int64, device=dev))
         rc = lib.sgcn_sgd_step(table.data_ptr(), numel_d.data_ptr(), chunks_d.data_ptr(),
                                nchunks, momentum, int(bool(g0["nesterov"])), _stream(table))
         _lib.check(rc, "sgcn_sgd_step")
