@@ -192,6 +192,8 @@ int main(int argc, char** argv) {
         fwd_variant<256, 128, 4, 1>(s, v, st, y2, fl, by);
         fwd_variant<256, 256, 4, 2>(s, v, st, y2, fl, by);
         fwd_variant<256, 64, 4, 2>(s, v, st, y2, fl, by);
+        // 4 waves of 128 x 128 (MI = NJ = 4: 128 B of LDS fragment reads per MFMA)
+        fwd_variant<256, 256, 2, 2>(s, v, st, y2, fl, by);
       }
     }
     if (do_dw) {
