@@ -344,6 +344,8 @@ def main():
             step()
         runner = g.replay
 
+    if sync is not None and not args.graph:
+        sync.timing(True)   # HIP events around each timed step's all_reduce
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -357,6 +359,13 @@ def main():
     rank_ms = [round(1000.0 * elapsed / args.steps, 3)]
     if distributed:
         elapsed, rank_ms = _max_over_ranks(elapsed, dev, world, args.steps)
+    comm = None
+    if sync is not None:
+        comm = sync.timing_summary()
+        sync.timing(False)
+        comm["allreduce_ms_per_step_max_over_ranks"] = (
+            None if comm["allreduce_ms_per_step"] is None else
+            _max_over_ranks(comm["allreduce_ms_per_step"], dev, world, 1)[0])
 
     clips = args.batch * world * args.steps
     value = clips / elapsed
@@ -461,7 +470,7 @@ def main():
                                    f"(fwd+CE+bwd+SGD), x=({args.batch},3,{T},{V},{M}) per GPU",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "hipgraph": bool(args.graph),
-                       **_ranks_info(distributed, world, rank_ms)},
+                       **_ranks_info(distributed, world, rank_ms), **_comm_info(comm)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
@@ -509,6 +518,17 @@ def _ranks_info(distributed, world, rank_ms):
     else:
         ws, be = 1, "none"
     return {"world_size": ws, "backend": be, "rank_ms_per_step": rank_ms}
+
+
+def _comm_info(comm):
+    """The gradient all-reduce of the timed steps (N > 1): HIP-event ms per step on this
+    rank and the max over ranks, the bucket's bytes and the bus GB/s (ring convention);
+    nulls at N = 1 (no collective) or under --graph (no events inside the capture)."""
+    if comm is None:
+        return {"allreduce_ms_per_step": None, "bucket_bytes": None,
+                "allreduce_bus_gbs": None}
+    return {k: comm[k] for k in ("allreduce_ms_per_step", "allreduce_ms_per_step_max_over_ranks",
+                                 "bucket_bytes", "allreduce_bus_gbs")}
 
 
 def _roofline(summ, n_iters, value_per_gpu, gflop_per_unit):

@@ -22,7 +22,7 @@ extern "C" {
 #endif
 
 #define SGCN_EINVAL (-22)
-#define SGCN_ABI_VERSION 22
+#define SGCN_ABI_VERSION 23
 /* Set in sgcn_abi_version()'s value by a diagnostic build (SGCN_PW_DIAG, SGCN_PW_STAMPS,
  * SGCN_DIAG_*: timing probes whose results are WRONG, `make diag` only); the Python loader
  * refuses such a library. */
@@ -39,7 +39,10 @@ extern "C" {
  * sgcn_bn_fold / sgcn_bn_bwd_fold and their consumers sgcn_tshift_fwd_fold,
  * sgcn_bn_apply_fold, sgcn_tshift_bwd_bnin_fold, sgcn_bn_bwd_apply_fold; the inference
  * epilogue sgcn_pw_fwd_bn_res; the CU-masked streams), and so are the fold structs in the
- * default kernels' argument lists. */
+ * default kernels' argument lists.
+ * 23: sgcn_sgd_step flags bit 2 (the (weight_decay, lr) column as the device address of a
+ * float pair: hyper-parameters of a graph-captured step read at replay); sgcn_pw_fwd_tshift
+ * takes two_row (the two-tap operand of channels with |xpos| < 2^-25). */
 int sgcn_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
@@ -206,14 +209,19 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
  * also store S there from the same registers (the weight gradient's operand, for
  * sgcn_pw_dw; NULL = not written). w is (M, K) k-contiguous (Conv2d
  * weight); relu != 0 applies ReLU. Workspace: sgcn_pw_tshift_ws_bytes(K) (the per-channel
- * shift table). */
+ * shift table + one flag word). two_row (ABI 23): 0 = four taps per element; 1 = when
+ * EVERY channel's xpos lies in (-2^-25, 0], two taps of the element's own column, rows
+ * floor(y) and floor(y)+1 (there the .cu:73 blend reduces to q21*(1-dy) + q22*dy exactly:
+ * bit-identical still); 2 = also when channels have 0 < xpos < 2^-25 (1 - dx rounds to 1;
+ * the dropped dx terms weigh < 2^-25: within 3e-8 * max|tap| of sgcn_tshift_fwd). A launch
+ * with any other channel uses four taps for all (decided on the device, per launch). */
 size_t sgcn_pw_tshift_ws_bytes(int K);
 int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long long x_bstride,
                        long long x_cstride, const float* xpos, const float* ypos,
                        const float* in_scale, const float* in_shift, float* x_shifted,
                        void* ws, size_t ws_bytes, float* y, long long y_bstride,
-                       long long y_cstride, int relu, int B, int M, int K, int T, int V,
-                       void* stream);
+                       long long y_cstride, int relu, int two_row, int B, int M, int K, int T,
+                       int V, void* stream);
 
 /* Workspace bytes for sgcn_pw_dw. */
 size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V);
@@ -410,7 +418,10 @@ int sgcn_sgd_chunk_elems(void);
  * | (float lr bits) << 32, flags (bit 0: the momentum buffer is new: initialised to the
  * step's d_p, torch's clone; bit 1: scale the gradient by the float whose bits are flags
  * bits 32-63 and store the scaled gradient back, i.e. GradAllReduce's deferred
- * `grad *= 1/world`)}; `numel` (device int32) per tensor; `chunks` (device int32)
+ * `grad *= 1/world`; bit 2 (ABI 23): the fourth column is instead the device address of a
+ * float pair {weight_decay, lr}, read by the kernel, so a graph-captured step follows
+ * learning-rate changes made between replays)}; `numel` (device int32) per tensor; `chunks`
+ * (device int32)
  * {tensor, first element} per chunk of at most sgcn_sgd_chunk_elems() elements. Per
  * element, torch's order: g = g*s (bit 1); d = g + wd*p (wd != 0); b = first ? d :
  * momentum*b + d (momentum != 0); d = nesterov ? d + momentum*b : b; p = p - lr*d. */

@@ -14,7 +14,11 @@
 // the gradient by the float in bits 32-63 first and store it back)} as int64, and a chunk
 // map {tensor, first element} per workgroup. The scale is the data-parallel reduction's
 // 1/world (shiftgcn/dist.py): the all-reduced SUM is scaled here instead of by a separate
-// pass between the all-reduce and the update.
+// pass between the all-reduce and the update. Flags bit 2 (ABI 23): the (weight_decay, lr)
+// column is instead the device address of that group's float pair, which the optimizer
+// keeps current (shiftgcn/train.py FusedSGD): a step captured in a hipGraph then reads the
+// learning rate of the replay, not the one of the capture (main.py:342-353 changes it per
+// epoch).
 #include "common.hpp"
 
 namespace sgcn {
@@ -36,8 +40,15 @@ __global__ __launch_bounds__(kSgdThreads) void sgd_step_kernel(
   // the gradient is read and (scaled) written back through one pointer: no __restrict__
   float* g = reinterpret_cast<float*>(e.g);
   float* __restrict__ buf = reinterpret_cast<float*>(e.buf);
-  const float wd = __uint_as_float((unsigned)(e.wdlr & 0xffffffffLL));
-  const float lr = __uint_as_float((unsigned)((unsigned long long)e.wdlr >> 32));
+  float wd, lr;
+  if (e.flags & 4) {                                   // device-resident hyper-parameters
+    const float* h = reinterpret_cast<const float*>(e.wdlr);
+    wd = h[0];
+    lr = h[1];
+  } else {
+    wd = __uint_as_float((unsigned)(e.wdlr & 0xffffffffLL));
+    lr = __uint_as_float((unsigned)((unsigned long long)e.wdlr >> 32));
+  }
   const bool first = (e.flags & 1) != 0;
   const bool scaled = (e.flags & 2) != 0;
   const float gs = __uint_as_float((unsigned)((unsigned long long)e.flags >> 32));

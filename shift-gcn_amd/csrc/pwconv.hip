@@ -24,6 +24,7 @@
 //      deterministic fp32 partial slabs [split][M][N] + row sums (bias grad), reduced in
 //      fixed order by slab_reduce_kernel (optionally transposed, for Linear_weight's
 //      (C_in, C_out) layout).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -181,7 +182,26 @@ __device__ __forceinline__ int rot_step(int d, int rsign, int V) { return pmod(d
 // plane, the .cu:73 blend in order, no contraction), so it is bit-identical to writing
 // the shifted tensor with sgcn_tshift_fwd and contracting it. Per-channel geometry comes
 // from a table (12 words per channel, 48-byte rows for scalar loads):
-//   [0] off = y1*V + x1, [1] y1, [2] x1, [3] dx, [4] dy, [5] a, [6] b
+//   [0] off = y1*V + x1, [1] y1, [2] x1, [3] dx, [4] dy, [5] a, [6] b,
+//   [7] two-row channel (below), [8] y1*V, [9] 1 - dy
+//
+// Two-row channels (round 6, verdict r05 x1). The blend of .cu:73 in float is
+//   q11*(1-dx)*(1-dy) + q21*dx*(1-dy) + q12*(1-dx)*dy + q22*dx*dy.
+// For x = xpos in (-2^-25, 0): x1 = -1 and dx = x + 1 rounds to exactly 1.0f, so 1-dx = 0,
+// q11 and q12 only add zeros and q21*dx = q21, q22*dx = q22: the value IS
+// q21*(1-dy) + q22*dy with q21, q22 on the element's own column. For x = 0: x1 = 0, dx = 0,
+// and it is q11*(1-dy) + q12*dy, the same two taps. Those channels (every channel of a
+// model whose xpos was initialised in U(-1e-8, 0], shift.py:39: its gradient is exactly
+// +-0, .cu:386, so only weight decay moves it, towards 0) need two taps of one column
+// instead of four: half the bytes returned into VGPRs and a third of the VALU, which on
+// gfx950 is what the fused operand costs against the fp32 MFMA (profiles/r05_dma2/).
+// Bit-identical to the four-tap form (up to the sign of an exact zero). With mode 2 the
+// channels with 0 < x < 2^-25 (1-dx rounds to 1) take it too, dropping the q21*dx and
+// q22*dx terms (|dx| < 3e-8: within 3e-8 * max|q| of the exact value, north_star's 1e-5).
+// The choice is per launch: the table kernel also writes one flag, set when EVERY channel
+// qualifies, which the contraction reads once at its start (a per-row choice costs a
+// scalar-load wait per operand row inside the main loop: measured 2x slower); a launch with
+// any other channel takes the four-tap form for all.
 // ------------------------------------------------------------------------------------
 constexpr int kTsWords = 12;
 
@@ -198,28 +218,51 @@ __device__ __forceinline__ float ts_blend(float q11, float q21, float q12, float
   return q11 * omdx * omdy + q21 * dx * omdy + q12 * omdx * dy + q22 * dx * dy;
 }
 
+// the two-row channels' blend: q21*(1-dy) + q22*dy (omdy = 1 - dy from the table)
+__device__ __forceinline__ float ts_blend2(float q0, float q1, float omdy, float dy) {
+#pragma clang fp contract(off)
+  return q0 * omdy + q1 * dy;
+}
+
 // per-channel table: x1 = floorf(x), dx = x - x1 (.cu:49-71), same for y (stride 1: no
 // +0.5, shift.py:17-18 applies to stride != 1 only)
 __global__ void tshift_params_kernel(const float* __restrict__ xpos,
                                      const float* __restrict__ ypos,
                                      const float* __restrict__ scale,
                                      const float* __restrict__ shift, int K, int V,
-                                     int* __restrict__ tab) {
+                                     int two_row, int* __restrict__ tab) {
 #pragma clang fp contract(off)
   SGCN_CRIT_PRIO();
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
   const float x = xpos[k], y = ypos[k];
   const int x1 = (int)floorf(x), y1 = (int)floorf(y);
+  const float dx = x - (float)x1, dy = y - (float)y1;
   int* r = tab + k * kTsWords;
   r[0] = y1 * V + x1;
   r[1] = y1;
   r[2] = x1;
-  r[3] = __float_as_int(x - (float)x1);
-  r[4] = __float_as_int(y - (float)y1);
+  r[3] = __float_as_int(dx);
+  r[4] = __float_as_int(dy);
   r[5] = __float_as_int(scale ? scale[k] : 1.f);
   r[6] = __float_as_int(shift ? shift[k] : 0.f);
-  for (int i = 7; i < kTsWords; ++i) r[i] = 0;
+  // two-row channel: exact (x1 = -1 with 1 - dx == 0, or dx == 0), or with mode 2 also
+  // x1 = 0 with 1 - dx == 1 (the dropped terms weigh dx < 2^-25)
+  const bool exact2 = (x1 == -1 && 1.f - dx == 0.f) || (x1 == 0 && dx == 0.f);
+  const bool approx2 = two_row >= 2 && x1 == 0 && 1.f - dx == 1.f;
+  r[7] = two_row >= 1 && (exact2 || approx2) ? 1 : 0;
+  r[8] = y1 * V;
+  r[9] = __float_as_int(1.f - dy);
+  for (int i = 10; i < kTsWords; ++i) r[i] = 0;
+}
+
+// the launch's two-row flag (tab[K * kTsWords]): every channel two-row (one workgroup)
+__global__ __launch_bounds__(256) void tshift_two_row_flag_kernel(int K,
+                                                                  int* __restrict__ tab) {
+  SGCN_CRIT_PRIO();
+  const int k = threadIdx.x;
+  const int all = __syncthreads_and(k >= K || tab[k * kTsWords + 7] != 0);
+  if (k == 0) tab[K * kTsWords] = all;
 }
 
 // ------------------------------------------------------------------------------------
@@ -279,6 +322,9 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   const auto ar = make_rsrc(p.A, p.a_bytes);
   const auto mr = make_rsrc(MASK ? p.mask : p.A, MASK ? p.mask_bytes : 0u);
   const auto xsr = make_rsrc(TSH && p.xs ? p.xs : p.A, TSH && p.xs ? p.x_bytes : 0u);
+  // TSH: every channel of the launch takes the two-row operand (the table's flag word)
+  const bool two =
+      TSH && ((const __attribute__((address_space(4))) int*)p.ts)[K * kTsWords] != 0;
 
   for (int i = tid; i < BM; i += NT) {
     bias_s[i] = (p.bias && m0 + i < M) ? p.bias[m0 + i] : 0.f;
@@ -332,21 +378,37 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   float ra[A_PER], rb[B_PER], rm[MASK ? B_PER : 1];
   float rq[TSH ? B_PER : 1][TSH ? 3 : 1];   // TSH: taps q21, q12, q22 (q11 in rb)
   const unsigned v4 = (unsigned)(V * 4);
-  auto load_stage = [&](int k0) {
-    int cv = cv0;
+  // TSH: the per-channel table through the constant address space, so its (wave-uniform)
+  // rows are fetched by scalar loads: as a plain global pointer the compiler cannot prove
+  // the kernel's own stores (the side output) leave it alone and issues VECTOR loads, each
+  // followed by a vmcnt(0) wait that drains every tap load in flight (round-6 ISA: the
+  // fused contraction ran at half its round-2 speed)
+  using cint = const __attribute__((address_space(4))) int;
+  cint* tsc = (cint*)p.ts;
+  auto load_tsh = [&](int k0) {
+    // taps of H around (t + y1, v + x1); a tap outside the plane is masked in store_stage
+    // (its address is clamped / past the extent, never faulting). An in-plane tap lies
+    // inside [0, x_bytes - 4 - row offset], so clamping every tap offset into that range
+    // only moves taps that store_stage masks, and no address (voffset + soffset) ever
+    // leaves the operand; a column past P keeps the out-of-range marker for all taps.
+    if constexpr (!TSH) return;
+    else if (two) {   // two-row channels: rows y1, y1 + 1 of the element's own column
 #pragma unroll
-    for (int i = 0; i < ((SGCN_PW_DIAG & 2) && k0 ? 0 : B_PER); ++i) {
-      const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
-      if (TSH) {
-        // four taps of H around (t + y1, v + x1); a tap outside the plane is masked in
-        // store_stage (its address is clamped / past the extent, never faulting)
-        // An in-plane tap lies inside [0, x_bytes - 4 - row offset], so clamping every
-        // tap offset into that range only moves taps that store_stage masks, and no
-        // address (voffset + soffset) ever leaves the operand; a column past P keeps the
-        // out-of-range marker for all four taps.
-        const int off = p.ts[row * kTsWords];
+      for (int i = 0; i < B_PER; ++i) {
+        const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
         const unsigned so = (unsigned)row * xcs4;
-        const int vo = (int)xcol + off * 4, lim = (int)(p.x_bytes - 4u - so);
+        const int vo = (int)xcol + tsc[row * kTsWords + 8] * 4;
+        const int lim = (int)(p.x_bytes - 4u - so);
+        rb[i] = bload(xr, colok ? (unsigned)min(max(vo, 0), lim) : p.x_bytes, so);
+        rq[i][1] = bload(xr, colok ? (unsigned)min(max(vo + (int)v4, 0), lim) : p.x_bytes, so);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
+        const unsigned so = (unsigned)row * xcs4;
+        const int vo = (int)xcol + tsc[row * kTsWords] * 4;
+        const int lim = (int)(p.x_bytes - 4u - so);
         auto tap = [&](int d) {
           return colok ? (unsigned)min(max(vo + d, 0), lim) : p.x_bytes;
         };
@@ -354,8 +416,15 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         rq[i][0] = bload(xr, tap(4), so);
         rq[i][1] = bload(xr, tap((int)v4), so);
         rq[i][2] = bload(xr, tap((int)v4 + 4), so);
-        continue;
       }
+    }
+  };
+  auto load_stage = [&](int k0) {
+    int cv = cv0;
+    if constexpr (TSH) load_tsh(k0);
+#pragma unroll
+    for (int i = 0; i < (TSH || ((SGCN_PW_DIAG & 2) && k0) ? 0 : B_PER); ++i) {
+      const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
       const unsigned voff = XROT ? xcol + (unsigned)(cv * 4) : xcol;
       rb[i] = bload_pol<SGCN_PW_XPOL>(xr, voff, (unsigned)row * xcs4);
       if (MASK) rm[i] = bload(mr, mcol, (unsigned)row * 4u);
@@ -372,24 +441,48 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
                                       ak0 + (unsigned)i * astep);
   };
   const int T = p.T;
-  auto store_stage = [&](int buf, int k0) {
+  // TSH: form the shifted operand from the taps (straight-line per form: a branch inside
+  // the unrolled loop left the tap arrays in scratch). The side output (the shifted operand
+  // itself, for the weight gradient; each element is formed exactly once when one M-block
+  // covers all M) is stored unconditionally: without x_shifted its descriptor has range 0.
+  auto store_tsh = [&](int buf, int k0) {
+    if constexpr (!TSH) return;
+    else if (two) {
 #pragma unroll
-    for (int i = 0; i < ((SGCN_PW_DIAG & 2) && k0 ? 0 : B_PER); ++i) {
-      float val = MASK ? rb[i] * rm[i] : rb[i];
-      if (TSH) {
+      for (int i = 0; i < B_PER; ++i) {
         const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
-        const int* pr = p.ts + row * kTsWords;
+        cint* pr = tsc + row * kTsWords;
+        const int tr = tt + pr[1];
+        const float a = __int_as_float(pr[5]), b = __int_as_float(pr[6]);
+        const bool r0 = (unsigned)tr < (unsigned)T, r1 = (unsigned)(tr + 1) < (unsigned)T;
+        const float val = ts_blend2(ts_tap(rb[i], a, b, r0), ts_tap(rq[i][1], a, b, r1),
+                                    __int_as_float(pr[9]), __int_as_float(pr[4]));
+        bstore(xsr, val, colok ? xcol : p.x_bytes, (unsigned)row * xcs4);
+        Bs[buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
+        cint* pr = tsc + row * kTsWords;
         const int tr = tt + pr[1], vr = vv + pr[2];
         const float a = __int_as_float(pr[5]), b = __int_as_float(pr[6]);
         const bool r0 = (unsigned)tr < (unsigned)T, r1 = (unsigned)(tr + 1) < (unsigned)T;
         const bool c0 = (unsigned)vr < (unsigned)V, c1 = (unsigned)(vr + 1) < (unsigned)V;
-        val = ts_blend(ts_tap(rb[i], a, b, r0 && c0), ts_tap(rq[i][0], a, b, r0 && c1),
-                       ts_tap(rq[i][1], a, b, r1 && c0), ts_tap(rq[i][2], a, b, r1 && c1),
-                       __int_as_float(pr[3]), __int_as_float(pr[4]));
-        // side output: the shifted operand itself, for the weight gradient (each element
-        // is formed exactly once when one M-block covers all M)
-        if (p.xs) bstore(xsr, val, colok ? xcol : p.x_bytes, (unsigned)row * xcs4);
+        const float val =
+            ts_blend(ts_tap(rb[i], a, b, r0 && c0), ts_tap(rq[i][0], a, b, r0 && c1),
+                     ts_tap(rq[i][1], a, b, r1 && c0), ts_tap(rq[i][2], a, b, r1 && c1),
+                     __int_as_float(pr[3]), __int_as_float(pr[4]));
+        bstore(xsr, val, colok ? xcol : p.x_bytes, (unsigned)row * xcs4);
+        Bs[buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
       }
+    }
+  };
+  auto store_stage = [&](int buf, int k0) {
+    if constexpr (TSH) store_tsh(buf, k0);
+#pragma unroll
+    for (int i = 0; i < (TSH || ((SGCN_PW_DIAG & 2) && k0) ? 0 : B_PER); ++i) {
+      const float val = MASK ? rb[i] * rm[i] : rb[i];
       Bs[AR ? 0 : buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
     }
     if (AR) return;
@@ -1429,15 +1522,16 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   return 0;
 }
 
-size_t sgcn_pw_tshift_ws_bytes(int K) { return (size_t)K * kTsWords * sizeof(int); }
+size_t sgcn_pw_tshift_ws_bytes(int K) { return ((size_t)K * kTsWords + 1) * sizeof(int); }
 
 int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long long x_bstride,
                        long long x_cstride, const float* xpos, const float* ypos,
                        const float* in_scale, const float* in_shift, float* x_shifted,
                        void* ws, size_t ws_bytes, float* y, long long y_bstride,
-                       long long y_cstride, int relu, int B, int M, int K, int T, int V,
-                       void* stream) {
+                       long long y_cstride, int relu, int two_row, int B, int M, int K, int T,
+                       int V, void* stream) {
   SGCN_REQUIRE(B >= 0 && M > 0 && K > 0 && K <= 256 && T >= 0 && V > 0 && V < 32768);
+  SGCN_REQUIRE(two_row >= 0 && two_row <= 2);
   SGCN_REQUIRE((in_scale == nullptr) == (in_shift == nullptr));
   SGCN_REQUIRE(x_cstride * (long long)K < (1LL << 31) && y_cstride * (long long)M < (1LL << 31));
   SGCN_REQUIRE(x_cstride >= (long long)T * V && y_cstride >= (long long)T * V);
@@ -1448,7 +1542,8 @@ int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long l
   SGCN_REQUIRE(w && x && y && xpos && ypos && ws && ws_bytes >= sgcn_pw_tshift_ws_bytes(K));
   hipStream_t st = (hipStream_t)stream;
   tshift_params_kernel<<<(K + 63) / 64, 64, 0, st>>>(xpos, ypos, in_scale, in_shift, K, V,
-                                                     (int*)ws);
+                                                     two_row, (int*)ws);
+  tshift_two_row_flag_kernel<<<1, 256, 0, st>>>(K, (int*)ws);
   SGCN_LAUNCH_CHECK();
   FwdArgs a{};
   a.A = w;
@@ -1471,7 +1566,14 @@ int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long l
   a.a_bytes = (unsigned)((long long)M * K * 4);
   a.mask_bytes = 0u;
   a.relu = relu ? 1 : 0;
+  // (A/B knob while measuring the round-6 two-row operand: SGCN_TSH_TILE=1 takes the
+  // plain path's 128 x 128 tile at 64 < M <= 128)
+  static const int tile_knob = [] {
+    const char* e = getenv("SGCN_TSH_TILE");
+    return e ? atoi(e) : 0;
+  }();
   if (M <= 64) launch_pwg_tsh<64, 256, 2, 4>(a, st);
+  else if (M <= 128 && tile_knob == 1) launch_pwg_tsh<128, 128, 4, 2>(a, st);
   else if (M <= 128) launch_pwg_tsh<128, 256, 2, 4>(a, st);
   else launch_pwg_tsh<256, 128, 4, 2>(a, st);
   SGCN_LAUNCH_CHECK();

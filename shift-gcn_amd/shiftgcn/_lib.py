@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # same-box A/B of two builds (tuning only, e.g. tools/ab_lib.sh): another in-tree build of
 # the same ABI
 LIB_PATH = os.environ.get("SGCN_LIB_PATH", LIB_PATH)
-ABI_VERSION = 22
+ABI_VERSION = 23
 BATCH_MAX = 32            # include/shiftgcn.h SGCN_BATCH_MAX
 ABI_DIAG_FLAG = 0x10000   # include/shiftgcn.h SGCN_ABI_DIAG_FLAG: a diagnostic build
 EINVAL = -22
@@ -52,7 +52,7 @@ SIGNATURES = {
                          _I, _I, _I, _I, _P]),
     "sgcn_pw_tshift_ws_bytes": (_Z, [_I]),
     "sgcn_pw_fwd_tshift": (_I, [_P, _P, _P, _L, _L, _P, _P, _P, _P, _P, _P, _Z, _P, _L, _L, _I,
-                                _I, _I, _I, _I, _I, _P]),
+                                _I, _I, _I, _I, _I, _I, _P]),
     "sgcn_pw_dw_ws_bytes": (_Z, [_I, _I, _I, _I, _I]),
     "sgcn_pw_dw": (_I, [_P, _L, _L, _I, _I, _P, _L, _L, _I, _I, _P, _P, _I, _I, _P, _I, _P, _Z,
                         _I, _I, _I, _I, _I, _P]),

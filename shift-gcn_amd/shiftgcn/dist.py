@@ -109,6 +109,8 @@ class GradAllReduce:
         if defer_scale_to is not None and not hasattr(defer_scale_to, "defer_grad_scale"):
             raise TypeError("defer_scale_to must be a shiftgcn.train.FusedSGD")
         self.copied = 0   # gradients copied into the bucket by the last call (diagnostics)
+        self.bucket_bytes = 4 * self.total
+        self._events = None   # [(start, end)] HIP events around each all_reduce (timing())
 
     def __call__(self):
         from . import ops
@@ -128,12 +130,40 @@ class GradAllReduce:
         self.copied = copied
         # the slots may be handed out again by the next backward (ops.grad_like)
         ops.release_grad_slots([p for _, p in self.named])
+        ev = self._events
+        if ev is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        if ev is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            ev.append((e0, e1))
         if self.defer_to is not None:
             self.defer_to.defer_grad_scale(
                 [(p, s) for (_, p), s in zip(self.named, self.param_scale) if s != 1.0])
         else:
             self.flat.mul_(self.scale)
+
+    def timing(self, on: bool = True):
+        """Start (clear) or stop recording HIP events on the current stream around every
+        all_reduce: from the moment the stream reaches the collective (its bucket written)
+        to the moment the reduced bucket is usable on it, i.e. what the step spends in the
+        collective, waiting for slower ranks included."""
+        self._events = [] if on else None
+
+    def timing_summary(self):
+        """{allreduce_ms_per_step, bucket_bytes, allreduce_bus_gbs, allreduce_calls} over the
+        recorded calls (after a device sync); bus GB/s = 2 (world - 1) / world x bytes / time,
+        the ring all-reduce convention of nccl-tests / rccl-tests."""
+        ev = self._events or []
+        if not ev:
+            return {"allreduce_ms_per_step": None, "bucket_bytes": self.bucket_bytes,
+                    "allreduce_bus_gbs": None, "allreduce_calls": 0}
+        ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        bus = 2.0 * (self.world - 1) / self.world * self.bucket_bytes / (ms * 1e-3) / 1e9
+        return {"allreduce_ms_per_step": round(ms, 4), "bucket_bytes": self.bucket_bytes,
+                "allreduce_bus_gbs": round(bus, 2), "allreduce_calls": len(ev)}
 
     def clip_grad_norm_(self, max_norm: float, eps: float = 1e-6):
         """``torch.nn.utils.clip_grad_norm_`` (2-norm) of the REDUCED gradients, right after

@@ -177,9 +177,23 @@ class Ensemble(nn.Module):
         return scores, acc
 
 
-def _state_key(module):
-    """Storage and version of every parameter and buffer of ``module``."""
-    return ops._src_key(list(module.parameters()) + list(module.buffers()))
+# submodule (re)registrations anywhere: EnsembleGraph re-lists the ensemble's modules
+_MODULE_EPOCH = [0]
+
+
+def _module_registered(*_):
+    _MODULE_EPOCH[0] += 1
+
+
+torch.nn.modules.module.register_module_module_registration_hook(_module_registered)
+
+
+def _state_key(mods):
+    """Storage and version of every parameter and buffer of the modules ``mods`` (read
+    from their own dicts, so a replaced parameter or buffer is seen; ~1 ms for the four
+    MediaPipe models against ~4.7 ms through ``module.parameters()``)."""
+    return [(t.data_ptr(), t._version) for m in mods for d in (m._parameters, m._buffers)
+            for t in d.values() if t is not None]
 
 
 class EnsembleGraph:
@@ -198,6 +212,7 @@ class EnsembleGraph:
         self.device = device
         self.static_in = torch.zeros(batch_shape, device=device, dtype=torch.float32)
         self.captures = 0
+        self._mods, self._epoch = list(ensemble.modules()), _MODULE_EPOCH[0]
         self._capture()
 
     def _capture(self):
@@ -212,11 +227,14 @@ class EnsembleGraph:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.scores, self.logits = ensemble(self.static_in)
-        self.key = _state_key(ensemble)
+        self.key = _state_key(self._mods)
         self.captures += 1
 
     def run(self, joint):
-        if _state_key(self.ensemble) != self.key:
+        if _MODULE_EPOCH[0] != self._epoch:   # a submodule was (re)registered somewhere
+            self._mods, self._epoch = list(self.ensemble.modules()), _MODULE_EPOCH[0]
+            self.key = None
+        if _state_key(self._mods) != self.key:
             self._capture()
         self.static_in.copy_(joint, non_blocking=True)
         self.graph.replay()

@@ -31,7 +31,6 @@ from __future__ import annotations
 
 import os
 import threading
-import weakref
 
 import torch
 
@@ -94,7 +93,6 @@ class _OffPath:
                 t.record_stream(self.side)
         self.ev = torch.cuda.Event()
         self.ev.record(self.side)
-        _SIDE_SEQ[self.side] = _SIDE_SEQ.get(self.side, 0) + 1
         return False
 
     def wait(self):
@@ -103,51 +101,128 @@ class _OffPath:
             torch.cuda.current_stream(self.tensors[0].device).wait_event(self.ev)
 
 
-# Optimizer-only finalizes of a backward on the side stream (position gradients, mask
-# gradients), deferred and launched together when the backward joins the side stream
-# (join_side): one launch per kind instead of one per unit (SGCN_BATCH_SIDE=0: each its own
-# side-stream launch, as before). Per device: {"pos": [...], "mask": [...]}.
+# --------------------------------------------------------------------------------------
+# Deferred gradient writes. A gradient written AFTER its block's backward has returned (a
+# weight gradient on the side stream, an optimizer-only finalize batched to the end of the
+# backward) is never handed to autograd: the block returns None for that parameter, and the
+# end-of-backward callback (_finish), once the side stream is joined, accumulates the tensor
+# into ``.grad`` itself, DDP-style. Autograd therefore never sums or copies an unwritten
+# tensor, whatever else contributes to the parameter's gradient in the same backward (a
+# regulariser in the loss, a parameter tied across blocks, the model used twice in one
+# graph, an existing ``.grad``). A parameter whose gradient autograd must see during the
+# backward (hooks, ``torch.autograd.grad`` capturing it, ``create_graph``) is not deferred.
+# --------------------------------------------------------------------------------------
+# Optimizer-only finalizes (position and mask gradients) are deferred to the end of the
+# backward and launched together: one launch per kind instead of one per unit
+# (SGCN_BATCH_SIDE=0: each its own launch, as before).
 BATCH_SIDE = int(os.environ.get("SGCN_BATCH_SIDE", "1"))
-_DEFER = {}
 
 
-def _deferred(device):
-    d = _DEFER.get(device)
-    if d is None:
-        d = _DEFER[device] = {"pos": [], "mask": []}
-    return d
+class _Later:
+    """A gradient tensor written after the block's backward returns (see above)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+
+def _late(t, off):
+    return _Later(t) if off else t
+
+
+class _Task:
+    """One backward pass's deferred work on one device: position / mask finalizes,
+    (parameter, gradient) pairs to accumulate, whether the side stream was used."""
+
+    __slots__ = ("pos", "mask", "grads", "side")
+
+    def __init__(self):
+        self.pos, self.mask, self.grads, self.side = [], [], [], False
+
+
+_TASKS = {}
+
+
+def _task(device):
+    """The current backward's _Task on ``device``; the first use queues its end-of-backward
+    callback (the engine runs final callbacks on the caller's stream, after every node)."""
+    key = (device, torch._C._current_graph_task_id())
+    t = _TASKS.get(key)
+    if t is None:
+        t = _TASKS[key] = _Task()
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _finish(key))
+    return t
+
+
+def _defer_ok(params):
+    """Whether the gradients of ``params`` may be written after the block's backward
+    returns: a plain backward that will run their AccumulateGrad (not
+    ``torch.autograd.grad`` capturing them, not ``backward(inputs=...)`` without them, not
+    ``create_graph``) and nothing that reads a gradient during the backward (tensor hooks,
+    post-accumulate-grad hooks)."""
+    if torch.is_grad_enabled():
+        return False   # create_graph: AccumulateGrad differentiates through the sum
+    for p in params:
+        if (getattr(p, "_backward_hooks", None) or
+                getattr(p, "_post_accumulate_grad_hooks", None)):
+            return False
+        try:
+            if not torch._C._will_engine_execute_node(
+                    torch.autograd.graph.get_gradient_edge(p).node):
+                return False
+        except RuntimeError:   # torch.autograd.grad returns p's gradient: not deferred
+            return False
+    return True
+
+
+def _accumulate(p, g):
+    """``.grad += g`` for a deferred gradient (AccumulateGrad's rule: take g when .grad is
+    None, else add in place), keeping p's gradient-bucket slot as .grad when g is it."""
+    cur = p.grad
+    if cur is None:
+        p.grad = g
+    elif ops.is_grad_slot(p, g) and not ops.is_grad_slot(p, cur):
+        g.add_(cur)        # (a + b == b + a bit for bit)
+        p.grad = g
+    else:
+        cur.add_(g)
+
+
+def _finish(key):
+    """End of a backward: the deferred finalizes (on the current stream before its wait
+    for the side stream, TAIL_MAIN bit 1, else on the side stream), the wait, then every
+    deferred gradient accumulated into its parameter's .grad."""
+    t = _TASKS.pop(key, None)
+    if t is None:
+        return
+    dev = key[0]
+    if t.pos or t.mask:
+        keep = [e[0].ws for e in t.pos] + [e[0] for e in t.mask]
+        with _OffPath(t.side and not (TAIL_MAIN & 1), *keep):
+            ops.pos_finalize_many(t.pos)
+            ops.mask_grad_finalize_many(t.mask)
+    s = _SIDE.get(dev)
+    if t.side and s is not None:
+        torch.cuda.current_stream(dev).wait_stream(s)
+    for p, g in t.grads:
+        _accumulate(p, g)
 
 
 def _pos_grads(gx, gy, shift):
     """A shift backward's (grad_xpos, grad_ypos): as returned, or, when its partials were
-    left for later (ops.PosPartials), finalized on the side stream into gradient tensors
-    allocated here (batched with the backward's others when BATCH_SIDE)."""
+    left for later (ops.PosPartials, a unit on the side stream), finalized after the
+    backward into gradient tensors allocated here (batched with the backward's others when
+    BATCH_SIDE) and handed over as deferred gradients."""
     if not isinstance(gx, ops.PosPartials):
         return gx, gy
     ox, oy = ops.grad_like(shift.xpos), ops.grad_like(shift.ypos)
     if BATCH_SIDE:
-        # written later through ALIASES: a reference to the returned tensor itself would
-        # raise its use count, and AccumulateGrad would then copy it before it is written
-        _deferred(gx.ws.device)["pos"].append((gx, ox.detach(), oy.detach()))
-        return ox, oy
-    with _OffPath(True, gx.ws):
-        gx.finalize(ox, oy)
-    return ox, oy
-
-
-def _flush_deferred(device, side=True):
-    """Launch the backward's deferred optimizer-only finalizes, on the side stream (after
-    everything enqueued on the current stream, which made their partials) or, for a
-    backward that did not use it, on the current stream."""
-    d = _DEFER.get(device)
-    if not d or not (d["pos"] or d["mask"]):
-        return
-    pos, mask = d["pos"], d["mask"]
-    d["pos"], d["mask"] = [], []
-    keep = [e[0].ws for e in pos] + [e[0] for e in mask]
-    with _OffPath(side, *keep):
-        ops.pos_finalize_many(pos)
-        ops.mask_grad_finalize_many(mask)
+        _task(gx.ws.device).pos.append((gx, ox, oy))
+    else:
+        with _OffPath(True, gx.ws):
+            gx.finalize(ox, oy)
+    return _Later(ox), _Later(oy)
 
 
 def _pos_alloc(shift, off):
@@ -163,50 +238,11 @@ def _pos_alloc(shift, off):
 TAIL_MAIN = int(os.environ.get("SGCN_TAIL_MAIN", "3"))
 
 
-# Side-stream launch groups enqueued (per side stream) and, per waiting stream, the count
-# it has already waited for: every linked unit queues a join, and a wait with nothing new
-# to wait for is one more barrier packet (≈ 5 µs) in front of the optimizer.
-_SIDE_SEQ = {}
-_JOINED = {}
-
-
-def join_side(device):
-    """Launch the deferred side-stream finalizes, then make the current stream wait for
-    every launch enqueued on the side stream (once: no wait when nothing new was enqueued
-    there since this stream's last join)."""
-    _flush_deferred(device, side=not (TAIL_MAIN & 1))
-    s = _SIDE.get(device)
-    if s is not None:
-        cur = torch.cuda.current_stream(device)
-        seq = _SIDE_SEQ.get(s, 0)
-        if _JOINED.get((cur, s)) != seq:
-            cur.wait_stream(s)
-            _JOINED[(cur, s)] = seq
-
-
 # ======================================================================================
 # Shift_gcn
 # ======================================================================================
 class GcnSaved:
-    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments", "shared",
-                 "__weakref__")
-
-
-def _register(mod, s):
-    """Record the forward state ``s`` of block ``mod`` among the block's live ones (weak:
-    one per graph that may yet run its backward). The deferred gradient writes (side stream,
-    end-of-backward finalizes) rely on autograd TAKING each returned gradient tensor as
-    ``.grad``; if the block's parameters get a second contribution in the same backward (the
-    block run twice in one graph), autograd sums the two tensors first — possibly before a
-    deferred launch has written one of them. So every state that was alive together with
-    another state of the same block is marked ``shared``, and its backward defers nothing."""
-    ws = mod.__dict__.get("_sgcn_live")
-    if ws is None:
-        ws = mod.__dict__["_sgcn_live"] = weakref.WeakSet()
-    s.shared = len(ws) > 0
-    for o in ws:
-        o.shared = True
-    ws.add(s)
+    __slots__ = ("x0", "xg", "Z", "zst", "D0", "dst", "H", "m", "h_moments")
 
 
 def gcn_forward(mod, x0, training, off=False):
@@ -247,7 +283,6 @@ def gcn_forward(mod, x0, training, off=False):
     s = GcnSaved()
     s.x0, s.xg, s.Z, s.zst, s.D0, s.dst, s.H, s.m = x0, xg, Z, zst, D0, dst, H, m
     s.h_moments = hm   # moments of H for Shift_tcn.bn, produced by the same launch
-    _register(mod, s)
     return H, s
 
 
@@ -329,7 +364,7 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
     with _OffPath(off, dZ, s.xg):
         ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
-    g["Linear_weight"], g["Linear_bias"] = dLW, dLb
+    g["Linear_weight"], g["Linear_bias"] = _late(dLW, off), _late(dLb, off)
     a2, a2m = extra_dx if isinstance(extra_dx, tuple) else (extra_dx, None)
     if prev is not None:   # also the previous unit's bn2 backward partials (x0 = its out)
         dx, mpart, extra_out["prev_part"] = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id,
@@ -338,28 +373,22 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     else:
         dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
     dmask = ops.grad_like(mod.Feature_Mask)
-    # (deferred only when autograd will TAKE dmask as .grad: an existing .grad, or a second
-    # contribution from another use of this block in the same graph, would be added to dmask
-    # before the deferred launch writes it)
     fm = mod.Feature_Mask
-    if (BATCH_SIDE and fm.grad is None and not s.shared and
-            not getattr(fm, "_backward_hooks", None) and
-            not getattr(fm, "_post_accumulate_grad_hooks", None) and
-            (off or _flush_queued(mpart.device))):
-        # with the backward's other optimizer-only finalizes (join_side / end of backward)
-        _deferred(mpart.device)["mask"].append((mpart, mod.Feature_Mask, B, Cin, V,
-                                                dmask.detach()))   # (alias: see _pos_grads)
+    if BATCH_SIDE and (off or _defer_ok((fm,))):
+        # with the backward's other optimizer-only finalizes (end of the backward)
+        _task(mpart.device).mask.append((mpart, fm, B, Cin, V, dmask))
+        g["Feature_Mask"] = _Later(dmask)
     else:
         with _OffPath(off, mpart):
-            ops.mask_grad_finalize(mpart, mod.Feature_Mask, B, Cin, V, out=dmask)
-    g["Feature_Mask"] = dmask
+            ops.mask_grad_finalize(mpart, fm, B, Cin, V, out=dmask)
+        g["Feature_Mask"] = _late(dmask, off)
     if mod.has_down:
         dWd = ops.grad_like(conv.weight)
         dbd = ops.grad_like(conv.bias)
         ops.pw_fwd(conv.weight, True, None, PV(dD0), PV(dx), Cin, Cout, T, V, accumulate=True)
         with _OffPath(off, dD0, x0):
             ops.pw_dw(PV(dD0), PV(x0), dWd, Cout, Cin, T, V, dbias=dbd)
-        g["down.0.weight"], g["down.0.bias"] = dWd, dbd
+        g["down.0.weight"], g["down.0.bias"] = _late(dWd, off), _late(dbd, off)
     return dx, g
 
 
@@ -462,7 +491,7 @@ def tcn_core_forward(mod, H, training, h_moments=None, tail=None, pre=None):
         # never read back; also stored from the same registers for the weight gradient
         As = torch.empty_like(H)
         ops.pw_fwd_tshift(tl.weight, tl.bias, PV(H), si.xpos.detach(), si.ypos.detach(), ast,
-                          PV(R), Cout, C, T, V, relu=True, x_shifted=As)
+                          PV(R), Cout, C, T, V, relu=True, x_shifted=As, two_row=TSHIFT_TWO_ROW)
     else:
         As = ops.tshift_fwd(H, si.xpos.detach(), si.ypos.detach(), si.stride, affine=ast)
         ops.pw_fwd(tl.weight, False, tl.bias, PV(As), PV(R), Cout, C, T, V, relu=True)
@@ -514,7 +543,7 @@ def tcn_core_backward(mod, s: TcnSaved, dS, materialize_dx=True, gpre=None, gcn_
     ops.pw_fwd(tl.weight, True, None, PV(dRp), PV(dAs), C, Cout, T, V)
     with _OffPath(off, dRp, s.As):   # after the dX contraction (see gcn_backward)
         ops.pw_dw(PV(dRp), PV(s.As), dWt, Cout, C, T, V, dbias=dbt)
-    g["temporal_linear.weight"], g["temporal_linear.bias"] = dWt, dbt
+    g["temporal_linear.weight"], g["temporal_linear.bias"] = _late(dWt, off), _late(dbt, off)
     # shift_in backward with Shift_tcn.bn's backward partials fused in (and, GBN, those of
     # the Shift_gcn BatchNorm that produced H)
     if gcn_z is not None and GBN_FUSION and si.stride == 1 and ops.ra_fits(T * V, V):
@@ -572,14 +601,14 @@ def convbn_dx_and_dw(mod, s: ConvBnSaved, dRc, dx, accumulate, off=False):
                accumulate=accumulate)
     with _OffPath(off, dRc, s.x):
         ops.pw_dw(PV(dRc), PV(s.x, mod.stride), dW, Cout, Cin, s.To, V, dbias=db)
-    return {"conv.weight": dW, "conv.bias": db}
+    return {"conv.weight": _late(dW, off), "conv.bias": _late(db, off)}
 
 
 # ======================================================================================
 # TCN_GCN_unit
 # ======================================================================================
 class UnitSaved:
-    __slots__ = ("x", "gs", "ts", "rs", "out", "prev", "off", "shared", "__weakref__")
+    __slots__ = ("x", "gs", "ts", "rs", "out", "prev", "off")
 
 
 def unit_forward(unit, x, training):
@@ -658,7 +687,6 @@ def unit_forward(unit, x, training):
     s = UnitSaved()
     s.x, s.gs, s.ts, s.rs, s.out, s.prev = x, gs, ts, rs, out, prev
     s.off = off
-    _register(unit, s)
     return out, s
 
 
@@ -671,38 +699,15 @@ def _gcn_z(unit, s: UnitSaved):
     return (s.gs.Z, s.gs.zst)
 
 
-def _flush_queued(device):
-    """In a backward without the side stream, queue (once per backward) the flush of the
-    deferred mask-gradient finalizes on the current stream at its end; False outside a
-    backward (nothing is deferred then)."""
-    if torch.is_grad_enabled():
-        return False   # create_graph backward: run in order
-    try:
-        torch.autograd.Variable._execution_engine.queue_callback(
-            lambda dev=device: _flush_deferred(dev, side=False))
-    except RuntimeError:
-        return False
-    return True
-
-
 def _off_path_ok(unit, s: UnitSaved):
-    """Weight gradients may run on the side stream only if autograd will take the returned
-    gradient tensors as they are (every .grad is None, so AccumulateGrad stores them
-    without launching anything on the current stream before the join)."""
-    if not s.off or torch.cuda.is_current_stream_capturing() or s.shared:
+    """Weight gradients (and position / mask finalizes) of a linked unit may run on the side
+    stream if every gradient of the unit may be deferred (_defer_ok): they are then handed
+    to .grad at the end of the backward, after the join."""
+    if not s.off or torch.cuda.is_current_stream_capturing():
         return False
-    if torch.is_grad_enabled():
-        # backward(create_graph=True): AccumulateGrad clones the gradient on the current
-        # stream instead of taking it, before the side stream would have written it
+    if not _defer_ok([p for p in unit.parameters() if p.requires_grad]):
         return False
-    for p in unit.parameters():
-        if p.requires_grad and (p.grad is not None or getattr(p, "_backward_hooks", None) or
-                                getattr(p, "_post_accumulate_grad_hooks", None)):
-            return False   # accumulation, or a hook that would read the gradient early
-    # join at the end of this backward pass, before backward() returns (the engine runs
-    # final callbacks on the caller's current stream)
-    torch.autograd.Variable._execution_engine.queue_callback(
-        lambda dev=s.x.device: join_side(dev))
+    _task(s.x.device).side = True
     return True
 
 
@@ -786,6 +791,10 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
 # two-launch form is faster at C = 256 too (+0.5 % same-box, profiles/r03_tsh/), so by
 # default no unit fuses (512 exceeds every Shift-GCN width). A/B knob (0 = every unit).
 TSHIFT_FUSION_MIN_C = int(os.environ.get("SGCN_TSHIFT_FUSION_MIN_C", "512"))
+# The fused operand's two-tap form for channels with |xpos| < 2^-25 (ops.pw_fwd_tshift
+# two_row; round 6): 2 = also 0 < xpos < 2^-25 (within 3e-8 x max|tap|), 1 = xpos in
+# (-2^-25, 0] only (bit-identical), 0 = four taps always. A/B knob.
+TSHIFT_TWO_ROW = int(os.environ.get("SGCN_TSHIFT_TWO_ROW", "2"))
 # Inference: the eval-mode BatchNorm right after a conv (down.1 after down.0, residual.bn
 # after residual.conv) folded into that conv's weights and bias (folded_conv_bn), so the
 # consumer adds the residual without an affine. A/B knob (round 4).
@@ -823,7 +832,8 @@ class _BlockFunction(torch.autograd.Function):
         training = module.training
         y, saved = fwd(module, x.contiguous(), training)
         ctx.impl, ctx.module, ctx.saved, ctx.training = impl, module, saved, training
-        ctx.names = [n for n, _ in trainable(module)]
+        tr = trainable(module)
+        ctx.names, ctx.params = [n for n, _ in tr], [p for _, p in tr]
         ctx.save_for_backward(x, y)
         return y
 
@@ -840,7 +850,14 @@ class _BlockFunction(torch.autograd.Function):
         _, bwd = ctx.impl
         dx, grads = bwd(ctx.module, ctx.saved, dy.contiguous())
         ctx.saved = None
-        return (None, None, dx) + tuple(grads.get(n) for n in ctx.names)
+        out = []
+        for n, p in zip(ctx.names, ctx.params):
+            g = grads.get(n)
+            if isinstance(g, _Later):   # written after this returns: accumulated by _finish
+                _task(g.t.device).grads.append((p, g.t))
+                g = None
+            out.append(g)
+        return (None, None, dx) + tuple(out)
 
 
 class _InferFlag(threading.local):

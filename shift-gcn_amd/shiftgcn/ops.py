@@ -136,6 +136,13 @@ def grad_slot(p):
     return flat[off:off + p.numel()].view(p.shape)
 
 
+def is_grad_slot(p, t):
+    """Whether ``t`` is p's bucket slot (the same memory)."""
+    s = _GRAD_SLOTS.get(p)
+    return (s is not None and t.data_ptr() == s[0].data_ptr() + 4 * s[1] and
+            t.numel() == p.numel())
+
+
 # slots handed out since the bucket's last release (GradAllReduce.__call__): a slot goes to
 # at most ONE gradient tensor per backward. A parameter with two gradient contributions in
 # one backward (the model called twice before one backward), or two torch.autograd.grad
@@ -183,23 +190,43 @@ def _cache_tensors(v):
     return tuple(t for x in v for t in _cache_tensors(x))
 
 
+# Set once a native writer of parameters or running statistics (FusedSGD.step, a training
+# BatchNorm finalize) has been captured in a hipGraph: a replay of that graph rewrites them
+# without advancing any version counter, so from then on the version-keyed eval caches
+# below are not trusted — every call recomputes its constants (inside a capture that puts
+# them into the graph, so a replayed eval reads current weights too).
+_CAPTURED_WRITES = False
+
+
+def mark_captured_writes():
+    global _CAPTURED_WRITES
+    _CAPTURED_WRITES = True
+
+
 def cached(owner, slot, key, make, device):
     """Value computed by ``make()`` once per ``key`` (storage + version of every tensor it
     reads), kept in ``owner.__dict__[slot]``: the eval-mode constants (BatchNorm apply
     coefficients, tanh(Feature_Mask) + 1) that change only when a weight or running
     statistic does. A stream that reads a cached tensor other than the one that made it is
     recorded on it (the caching allocator then keeps its memory until that stream is done
-    when the entry is replaced)."""
+    when the entry is replaced). Nothing is stored during a hipGraph capture (the value
+    would stay unwritten until the first replay), and nothing is cached at all once a
+    training step's writers were captured (mark_captured_writes)."""
+    if _CAPTURED_WRITES:
+        owner.__dict__.pop(slot, None)
+        return make()
     c = owner.__dict__.get(slot)
     cur = torch.cuda.current_stream(device)
+    capturing = torch.cuda.is_current_stream_capturing()
     if c is not None and c[0] == key:
-        if cur not in c[2] and not torch.cuda.is_current_stream_capturing():
+        if cur not in c[2] and not capturing:
             for t in _cache_tensors(c[1]):
                 t.record_stream(cur)
             c[2].add(cur)
         return c[1]
     v = make()
-    owner.__dict__[slot] = (key, v, {cur})
+    if not capturing:
+        owner.__dict__[slot] = (key, v, {cur})
     return v
 
 
@@ -590,12 +617,14 @@ def pw_dw(g: PlaneView, x: PlaneView, dw, M, Nc, T, V, mask=None, transpose=Fals
 
 
 def pw_fwd_tshift(w, bias, x: PlaneView, xpos, ypos, st, out: PlaneView, M, K, T, V,
-                  relu=False, x_shifted=None):
+                  relu=False, x_shifted=None, two_row=2):
     """Shift_tcn's shift_in fused into temporal_linear (sgcn_pw_fwd_tshift):
     out = act(w @ shift(st.scale*x + st.shift) + bias); the shifted operand is formed while
     staging and never read back (``x_shifted``: optionally stored, layout of x, for the
     weight gradient). ``st``: the BnStats of Shift_tcn.bn (None = identity); w is (M, K)
-    k-contiguous."""
+    k-contiguous. ``two_row``: 0 = every channel from four taps (bit-identical to
+    tshift_fwd); 1 = channels with xpos in (-2^-25, 0] from two taps of their own column
+    (still bit-identical); 2 = also 0 < xpos < 2^-25 (within 3e-8 * max|tap|)."""
     check_input(w, "weight")
     _opt(bias, "bias")
     if x.tstride != 1 or x.rsign != 0 or out.tstride != 1 or out.rsign != 0:
@@ -622,7 +651,8 @@ def pw_fwd_tshift(w, bias, x: PlaneView, xpos, ypos, st, out: PlaneView, M, K, T
                                         x.bstride, x.cstride, _ptr(xpos), _ptr(ypos), _ptr(sc),
                                         _ptr(sh), xs, _ptr(ws), nbytes,
                                         out.t.data_ptr() + 4 * b0 * out.bstride, out.bstride,
-                                        out.cstride, int(relu), nb, M, K, T, V, _stream(x.t))
+                                        out.cstride, int(relu), int(two_row), nb, M, K, T, V,
+                                        _stream(x.t))
             _lib.check(rc, "sgcn_pw_fwd_tshift")
     return out.t
 
@@ -674,6 +704,8 @@ def bn_finalize(part, B, F, n_part, bn, perm_V=0, training=True):
     _lib.check(rc, "sgcn_bn_finalize")
     if track:   # the running statistics were written in place by the kernel
         bump_versions((bn.running_mean, bn.running_var, bn.num_batches_tracked))
+        if torch.cuda.is_current_stream_capturing():
+            mark_captured_writes()
     return st
 
 

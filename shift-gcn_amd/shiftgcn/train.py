@@ -38,6 +38,23 @@ def merged_param_groups(model: torch.nn.Module, base_lr: float):
     return [{"params": ps, "lr": base_lr, "weight_decay": wd} for wd, ps in by_wd.items()]
 
 
+class _HyperGroup(dict):
+    """A FusedSGD parameter group: assigning its ``lr`` / ``weight_decay`` (what
+    :func:`adjust_learning_rate` and torch's LR schedulers do) also updates the optimizer's
+    device-resident copy, the one a graph-captured step reads at replay."""
+
+    __slots__ = ("_opt",)
+
+    def __init__(self, group, opt):
+        super().__init__(group)
+        self._opt = opt
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        if k in ("lr", "weight_decay"):
+            self._opt._hyper_changed(self)
+
+
 class FusedSGD(torch.optim.SGD):
     """``torch.optim.SGD`` (same constructor, param groups, hyper-parameters and state:
     ``state[p]["momentum_buffer"]``, so ``state_dict`` / ``load_state_dict`` round-trip with
@@ -46,7 +63,13 @@ class FusedSGD(torch.optim.SGD):
     Same arithmetic in the same order as torch's single/multi-tensor SGD (weight decay,
     momentum with the first-step clone, nesterov, update); groups must share momentum,
     dampening 0, nesterov and not maximize — otherwise, and for CPU or non-fp32
-    parameters, the stock ``step`` runs. Closures are supported as in torch."""
+    parameters, the stock ``step`` runs. Closures are supported as in torch.
+
+    Under hipGraph capture the launch reads each group's (weight_decay, lr) from a device
+    pair the optimizer keeps current (``sgcn_sgd_step`` flags bit 2): assigning
+    ``group["lr"]`` between replays (``adjust_learning_rate``, an LR scheduler) writes it
+    on the current stream, so the next replay uses the new value (main.py:342-353).
+    ``momentum`` / ``nesterov`` are launch arguments and stay those of the capture."""
 
     def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0,
                  nesterov=False, **kw):
@@ -56,6 +79,43 @@ class FusedSGD(torch.optim.SGD):
         self._layout = None   # (param signature, device numel / chunk map, n chunks)
         self._gscale = {}     # id(param) -> (param, gradient scale) for the next step only
         self._cap = None      # (pinned table buffer, device table) for a step under capture
+        self._hyper = None    # device (groups, 2) float32 {weight_decay, lr}, and its host mirror
+        self._hyper_host = None
+
+    def add_param_group(self, param_group):
+        super().add_param_group(param_group)
+        self._wrap_groups()
+
+    def __setstate__(self, state):   # (also what load_state_dict installs new groups with)
+        super().__setstate__(state)
+        self._wrap_groups()
+
+    def _wrap_groups(self):
+        pg = self.param_groups
+        for i, g in enumerate(pg):
+            if not isinstance(g, _HyperGroup):
+                pg[i] = _HyperGroup(g, self)
+        h = getattr(self, "_hyper", None)
+        if h is not None:
+            if h.shape[0] != len(pg):
+                self._hyper = self._hyper_host = None   # re-made by the next eager step
+            else:
+                for g in pg:
+                    self._hyper_changed(g)
+
+    def _hyper_changed(self, group):
+        """Write ``group``'s (weight_decay, lr) into the device pair (current stream)."""
+        h = getattr(self, "_hyper", None)
+        if h is None:
+            return
+        for i, g in enumerate(self.param_groups):
+            if g is group:
+                v = (float(g["weight_decay"]), float(g["lr"]))
+                if self._hyper_host[i] != v:
+                    h[i, 0].fill_(v[0])
+                    h[i, 1].fill_(v[1])
+                    self._hyper_host[i] = v
+                return
 
     def defer_grad_scale(self, pairs):
         """[(param, s)]: the next ``step`` first scales these parameters' gradients by s
@@ -119,10 +179,21 @@ class FusedSGD(torch.optim.SGD):
                             torch.tensor(chunks, dtype=torch.int32, device=dev),
                             len(chunks) // 2)
         _, numel_d, chunks_d, nchunks = self._layout
+        capturing = torch.cuda.is_current_stream_capturing()
+        if capturing:
+            # the launch reads (weight_decay, lr) from the device pairs at every replay
+            if (self._hyper is None or self._hyper.device != dev or
+                    any(hh != (float(g["weight_decay"]), float(g["lr"]))
+                        for hh, g in zip(self._hyper_host, self.param_groups))):
+                raise RuntimeError("FusedSGD: run one eager step before capturing a graph "
+                                   "(and set lr / weight_decay by item assignment)")
         rows = []
-        for g in self.param_groups:
-            wdlr = struct.unpack("<q", struct.pack("<ff", float(g["weight_decay"]),
-                                                  float(g["lr"])))[0]
+        for gi, g in enumerate(self.param_groups):
+            if capturing:
+                wdlr = self._hyper[gi].data_ptr()
+            else:
+                wdlr = struct.unpack("<q", struct.pack("<ff", float(g["weight_decay"]),
+                                                      float(g["lr"])))[0]
             for p in g["params"]:
                 if p.grad is None:
                     continue
@@ -132,7 +203,7 @@ class FusedSGD(torch.optim.SGD):
                     st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.preserve_format)
                     first = 1
                 buf = st.get("momentum_buffer") if momentum != 0 else p
-                flags = first
+                flags = first | (4 if capturing else 0)
                 sc = gscale.get(id(p))
                 if sc is not None and sc[0] is p:
                     # bit 1 + the float's bits in 32-63 (a signed int64 for the table)
@@ -140,21 +211,30 @@ class FusedSGD(torch.optim.SGD):
                     flags |= 2 | (bits << 32)
                     flags = struct.unpack("<q", struct.pack("<Q", flags))[0]
                 rows += [p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), wdlr, flags]
-        if torch.cuda.is_current_stream_capturing():
+        if capturing:
             # hipGraph capture (bench.py --graph): no host allocation is allowed here, so the
             # table goes through a pinned buffer and device table set up by an eager step;
             # the captured copy re-reads the buffer at every replay (same addresses: the
-            # graph's gradients and buffers are static)
+            # graph's gradients and buffers are static; the hyper-parameters are read through
+            # the device pairs, flags bit 2)
             if self._cap is None or self._cap[0].numel() != len(rows):
                 raise RuntimeError("FusedSGD: run one eager step before capturing a graph")
             host, table = self._cap
             host.numpy()[:] = rows
             table.copy_(host, non_blocking=True)
+            from . import ops
+            ops.mark_captured_writes()   # the eval caches cannot see replayed updates
         else:
             table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
             if self._cap is None or self._cap[0].numel() != len(rows):
                 self._cap = (torch.empty(len(rows), dtype=torch.int64).pin_memory(),
                              torch.empty(len(rows), dtype=torch.int64, device=dev))
+            if self._hyper is None or self._hyper.device != dev:
+                self._hyper = torch.empty((len(self.param_groups), 2), dtype=torch.float32,
+                                          device=dev)
+                self._hyper_host = [None] * len(self.param_groups)
+            for g in self.param_groups:   # (a no-op unless a value changed without a hook)
+                self._hyper_changed(g)
         rc = lib.sgcn_sgd_step(table.data_ptr(), numel_d.data_ptr(), chunks_d.data_ptr(),
                                nchunks, momentum, int(bool(g0["nesterov"])), _stream(table))
         _lib.check(rc, "sgcn_sgd_step")

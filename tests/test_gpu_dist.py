@@ -133,6 +133,14 @@ def test_bench_two_ranks_same_device():
     assert d["config"]["world_size"] == 2 and d["config"]["backend"] == "gloo"
     rm = d["config"]["rank_ms_per_step"]
     assert len(rm) == 2 and abs(max(rm) - d["ms_per_step"]) < 1e-2, (rm, d["ms_per_step"])
+    # the line explains its collective (HIP events around each timed
+    # step's all_reduce, the bucket's bytes, the ring bus rate)
+    c = d["config"]
+    assert c["bucket_bytes"] == 4 * 693_107
+    assert 0 < c["allreduce_ms_per_step"] <= c["allreduce_ms_per_step_max_over_ranks"]
+    assert c["allreduce_ms_per_step_max_over_ranks"] < d["ms_per_step"]
+    want = 2 * 1 / 2 * c["bucket_bytes"] / (c["allreduce_ms_per_step"] * 1e-3) / 1e9
+    assert abs(c["allreduce_bus_gbs"] - want) <= 0.01 * want + 0.01
 
 
 def _free_port():

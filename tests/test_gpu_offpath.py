@@ -6,8 +6,11 @@
 * Autograd takes the side-stream gradient tensors as they are: each weight gradient
   produced by a contraction IS the parameter's ``.grad`` afterwards (no clone launched on
   the current stream before the join).
-* ``.grad`` already set (gradient accumulation) falls back to the in-order path, and the
-  accumulated result equals two synchronous backward passes.
+* ``.grad`` already set (gradient accumulation), a regulariser term in the loss, a
+  parameter tied across two units, the data-parallel bucket, ``torch.autograd.grad`` and
+  ``backward(inputs=...)``: the deferred gradients (never handed to autograd, accumulated
+  into ``.grad`` at the end of the backward, ``fused._finish``) give exactly the in-order
+  path's gradients.
 """
 import pytest
 import torch
@@ -310,3 +313,130 @@ def test_two_autograd_grad_calls_get_distinct_slots():
     finally:
         ops.unregister_grad_slots(ps)
         ops.release_grad_slots(ps)
+
+
+_REG = ("Linear_weight", "Feature_Mask", "ypos", "conv.weight", "temporal_linear.weight",
+        "down.0.weight")
+
+
+def _extra_grads(dev, mode, variant, slots=False):
+    """Gradients of one step whose parameters also get a contribution from OUTSIDE their
+    unit: ``l2`` = CE + 1e-3 * sum ||p||^2 over the Linear / mask / ypos / conv weights,
+    ``tied`` = l3's Linear_weight IS l2's, ``tied_l2`` = both. ``mode`` 1 = side stream and
+    deferred finalizes, 0 = everything in order."""
+    from shiftgcn import fused
+    from shiftgcn.dist import GradAllReduce
+    old = fused.ASYNC_DW, fused.BATCH_SIDE
+    fused.ASYNC_DW = fused.BATCH_SIDE = mode
+    ga = None
+    try:
+        m = _model(dev)
+        if variant.startswith("tied"):
+            m.l3.gcn1.Linear_weight = m.l2.gcn1.Linear_weight
+        if slots:
+            ga = GradAllReduce(m)
+        x = formula.tensor((4, 3, 64, 25, 2), 48, 1.0).to(dev)
+        y = torch.tensor([0, 4, 2, 9], device=dev)
+        for p in m.parameters():
+            p.grad = None
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        if variant.endswith("l2"):
+            reg = [p for n, p in m.named_parameters() if n.endswith(_REG)]
+            assert len(reg) > 40
+            loss = loss + 1e-3 * sum(p.square().sum() for p in reg)
+        loss.backward()
+        if ga is not None:
+            ga()
+            # every gradient is (still) its bucket slot
+            assert all(ops_is_slot(p) for _, p in ga.named)
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()
+                if p.grad is not None}
+    finally:
+        fused.ASYNC_DW, fused.BATCH_SIDE = old
+        if ga is not None:
+            ga.close()
+
+
+def ops_is_slot(p):
+    from shiftgcn import ops
+    return p.grad is not None and ops.is_grad_slot(p, p.grad)
+
+
+@pytest.fixture
+def gloo_world1():
+    import socket
+
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1)
+    try:
+        yield
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variant", ["l2", "tied", "tied_l2"])
+def test_gradient_from_outside_the_unit_bit_identical(variant):
+    """a parameter whose gradient also comes from outside its
+    unit (a loss regulariser, a tied parameter). The side stream and the deferred finalizes
+    must give the in-order path's gradients bit for bit."""
+    dev = torch.device("cuda:0")
+    ref = _extra_grads(dev, 0, variant)
+    got = _extra_grads(dev, 1, variant)
+    assert got.keys() == ref.keys() and len(got) > 100
+    for n in ref:
+        assert torch.equal(got[n], ref[n]), n
+    if variant.endswith("l2"):   # the regulariser really reached those gradients
+        plain = _extra_grads(dev, 0, "tied" if variant == "tied_l2" else "none")
+        assert not torch.equal(plain["l2.gcn1.Feature_Mask"], ref["l2.gcn1.Feature_Mask"])
+
+
+@pytest.mark.parametrize("variant", ["l2", "tied_l2"])
+def test_gradient_from_outside_the_unit_with_bucket(variant, gloo_world1):
+    """The same with the data-parallel gradient bucket registered (GradAllReduce, world 1):
+    identical gradients, and every .grad is its bucket slot after the reduction."""
+    dev = torch.device("cuda:0")
+    ref = _extra_grads(dev, 0, variant, slots=True)
+    got = _extra_grads(dev, 1, variant, slots=True)
+    assert got.keys() == ref.keys()
+    for n in ref:
+        assert torch.equal(got[n], ref[n]), n
+    plain = _extra_grads(dev, 0, variant)
+    for n in ref:
+        assert torch.equal(got[n], plain[n]), n
+
+
+def test_autograd_grad_and_backward_inputs_in_order():
+    """``torch.autograd.grad`` over some parameters and ``backward(inputs=...)`` with the side
+    stream on: the units whose gradients are captured or not accumulated run in order, and
+    the results equal the in-order path's."""
+    from shiftgcn import fused
+    dev = torch.device("cuda:0")
+    x = formula.tensor((4, 3, 64, 25, 2), 49, 1.0).to(dev)
+    y = torch.tensor([1, 1, 2, 3], device=dev)
+    names = ("l4.gcn1.Linear_weight", "l7.tcn1.shift_in.ypos", "l2.gcn1.Feature_Mask",
+             "l9.tcn1.temporal_linear.weight")
+    res = {}
+    for mode in (0, 1):
+        old = fused.ASYNC_DW, fused.BATCH_SIDE
+        fused.ASYNC_DW = fused.BATCH_SIDE = mode
+        try:
+            m = _model(dev)
+            ps = [m.get_parameter(n) for n in names]
+            g = torch.autograd.grad(torch.nn.functional.cross_entropy(m(x), y), ps)
+            for p in m.parameters():
+                p.grad = None
+            torch.nn.functional.cross_entropy(m(x), y).backward(inputs=ps[:2])
+            torch.cuda.synchronize()
+            assert all(p.grad is None for n, p in m.named_parameters()
+                       if n not in names[:2])
+            res[mode] = ([t.cpu() for t in g], [p.grad.cpu() for p in ps[:2]])
+        finally:
+            fused.ASYNC_DW, fused.BATCH_SIDE = old
+        assert not fused._TASKS
+    for a, b in zip(res[0][0] + res[0][1], res[1][0] + res[1][1]):
+        assert torch.equal(a, b)

@@ -125,3 +125,66 @@ def test_training_step_has_no_shift_in_launch(monkeypatch, min_c):
     unfused = sum(getattr(m, f"l{k}").tcn1.in_channels < fused.TSHIFT_FUSION_MIN_C
                   for k in range(1, 11))
     assert calls == {"affine": unfused, "plain": 10}, calls
+
+
+def _tiny_x_inputs(B, K, M, T, V, seed, sign):
+    """xpos all within 2^-25 of 0 (the two-row operand's channels): ``sign`` -1 = all in
+    (-2^-25, 0] (exact), 0 = both signs, as shift.py:39's U(-1e-8, 1e-8) init gives."""
+    h, w, bias, _, ypos, scale, shift = _inputs(B, K, M, T, V, seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    xpos = (torch.rand(K, generator=g) - 0.5) * 2e-8
+    if sign < 0:
+        xpos = -xpos.abs()
+    edge = [-2.0 ** -25, -0.0, 0.0, -1e-30]
+    if sign >= 0:
+        edge += [2.0 ** -26, 1e-30]
+    xpos[3:3 + len(edge)] = torch.tensor(edge)
+    ypos[10], ypos[11] = 2.0, -1.0                            # integer shifts (dy = 0)
+    return h, w, bias, xpos.to(DEV), ypos, scale, shift
+
+
+TWO_ROW_CASES = [(3, 64, 64, 20, 25), (2, 128, 128, 17, 25), (2, 256, 256, 9, 25),
+                 (3, 64, 64, 11, 33)]
+
+
+@pytest.mark.parametrize("case", TWO_ROW_CASES, ids=["x".join(map(str, c)) for c in TWO_ROW_CASES])
+def test_two_row_operand(case):
+    """channels with |xpos| < 2^-25 take the two-tap operand
+    (rows floor(y), floor(y)+1 of the element's own column). two_row = 1 on xpos <= 0:
+    bit-identical to sgcn_tshift_fwd + sgcn_pw_fwd and to the oracle (.cu:49-73 with
+    1 - dx == 0); two_row = 2 with both signs: the xpos <= 0 channels still bit-exact vs the
+    oracle, the others within 2e-7 x max|tap| (the dropped dx terms weigh < 2^-25 each, plus
+    one rounding of the sum; north_star's bar is 1e-5); two_row 0: four taps."""
+    from oracle import shift_oracle as so
+    from shiftgcn import ops
+    from shiftgcn.ops import PlaneView as PV
+    B, K, M, T, V = case
+    for sign, mode in ((-1, 1), (0, 2), (0, 1), (0, 0)):
+        h, w, bias, xpos, ypos, scale, shift = _tiny_x_inputs(*case, seed=sum(case), sign=sign)
+        As = ops.tshift_fwd(h, xpos, ypos, 1, scale=scale, shift=shift)
+        r1 = torch.empty(B, M, T, V, device=DEV)
+        ops.pw_fwd(w, False, bias, PV(As), PV(r1), M, K, T, V, relu=True)
+        r2 = torch.empty(B, M, T, V, device=DEV)
+        xs = torch.full_like(h, float("nan"))
+        ops.pw_fwd_tshift(w, bias, PV(h), xpos, ypos, _St(scale, shift), PV(r2), M, K, T, V,
+                          relu=True, x_shifted=xs, two_row=mode)
+        r3 = torch.empty(B, M, T, V, device=DEV)   # the contraction of its own operand
+        ops.pw_fwd(w, False, bias, PV(xs), PV(r3), M, K, T, V, relu=True)
+        torch.cuda.synchronize()
+        assert torch.equal(r2, r3), (sign, mode)
+        # the oracle: bn affine per element (float32 multiply, then add), then the shift
+        hn, sc, sh = h.cpu().numpy(), scale.cpu().numpy(), shift.cpu().numpy()
+        aff = (hn * sc[None, :, None, None]).astype(np.float32) + sh[None, :, None, None]
+        want = so.shift_forward(aff.astype(np.float32), xpos.cpu().numpy(), ypos.cpu().numpy(), 1)
+        got = xs.cpu().numpy()
+        xn = xpos.cpu().numpy()
+        le0 = xn <= 0
+        assert np.array_equal(got[:, le0], want[:, le0]), (sign, mode)
+        if mode == 2:
+            assert not le0.all()
+            err = np.abs(got - want).max() / np.abs(aff).max()
+            assert err <= 2e-7, err
+            assert (np.abs(r2 - r1).max() / r1.abs().max()).item() <= 1e-5
+        else:   # exact: every channel, and the contraction too
+            assert np.array_equal(got, want), (sign, mode)
+            assert torch.equal(r1, r2), (sign, mode)

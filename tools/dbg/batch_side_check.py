@@ -26,7 +26,7 @@ for batch in (0, 1):
     y.backward(g)
     torch.cuda.synchronize()
     res[batch] = {n: p.grad.clone() for n, p in ours.named_parameters() if p.grad is not None}
-    print("batch", batch, "deferred left:", {k: (len(v["pos"]), len(v["mask"])) for k, v in fused._DEFER.items()})
+    print("batch", batch, "deferred left:", {k: (len(v.pos), len(v.mask)) for k, v in fused._TASKS.items()})
 for n in res[0]:
     d = (res[0][n] - res[1][n]).abs().max().item()
     if d > 0:
