@@ -877,6 +877,9 @@ __global__ __launch_bounds__(NT) void gcn_dx_finish_ja_kernel(
     const float* __restrict__ pmean, const float* __restrict__ pinvstd,
     float2* __restrict__ bn_part, int C, int T, int V, const float* __restrict__ add2m) {
   SGCN_CRIT_PRIO();
+#ifdef SGCN_DIAG_F1B_REAL
+  return;   // timing diagnostic only: the pass is fused into the contraction (pwconv.hip)
+#endif
   __shared__ float s0[NT];
   __shared__ float red[2 * NT / 64];
   const int plane = blockIdx.x, c = plane % C, rc = c % V;
@@ -893,7 +896,14 @@ __global__ __launch_bounds__(NT) void gcn_dx_finish_ja_kernel(
   float gv[LPT], xq[LPT], a1[ADD1 ? LPT : 1], a2[ADD2 ? LPT : 1], a2q[A2M ? LPT : 1];
   float sv[PART ? LPT : 1];
   {
+#ifdef SGCN_DIAG_F1B_BOUND
+    // timing diagnostic only (results wrong): dXt is never read (range 0), with the gcn dX
+    // contraction's stores dropped (pwconv.hip): the bound of fusing this pass into that
+    // contraction's epilogue (verdict r05, next #5)
+    const auto gr = make_rsrc(dxt + off, 0u), xr = make_rsrc(x0 + off, pb);
+#else
     const auto gr = make_rsrc(dxt + off, pb), xr = make_rsrc(x0 + off, pb);
+#endif
 #pragma unroll
     for (int e = 0; e < LPT; ++e) {
       gv[e] = bload(gr, uo + e * vstep, 0);

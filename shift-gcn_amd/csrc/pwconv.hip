@@ -91,6 +91,9 @@ struct FwdArgs {
   // extent loads 0 / drops the store) and epilogue flags
   unsigned x_bytes, y_bytes, a_bytes, mask_bytes;
   int relu;
+#ifdef SGCN_DIAG_F1B_REAL
+  int diag_f1b;
+#endif
 };
 
 // the FastDiv constants of a.T * a.V and a.V (every FwdArgs launch sets them)
@@ -598,7 +601,16 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   // the global load an output element needs besides the accumulator (ACCUM: the old
   // value) is issued for all of this wave's rows of a pass BEFORE the pass's LDS staging: in
   // the store loop it would wait a memory round trip (a load after the previous row's stores)
+#ifdef SGCN_DIAG_F1B_REAL
+  // timing diagnostic only (results wrong): the gcn input-gradient contraction's epilogue
+  // also reads three more tensors per element (what gcn_dx_finish's work would read there:
+  // x0, the residual gradient and its mask / the previous BatchNorm's input), see sgcn_pw_fwd
+  constexpr int NPF = ACCUM ? 4 : 0;
+  const int npf = p.diag_f1b ? 4 : 1;
+#else
   constexpr int NPF = ACCUM ? 1 : 0;
+  constexpr int npf = 1;
+#endif
   float pf[NPF ? RPW : 1][NPF ? CQ : 1][NPF ? NPF : 1];
   auto row_of = [&](int i, int h, int k) {   // (tile row, its store row offset)
     const int lr = wid + k * NW;
@@ -633,6 +645,10 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
               const int vo = voff_of(trow, q);
               const unsigned voff = ycolq[q] + (unsigned)(vo * 4);
               pf[k][q][0] = bload(yr, voff, soff);
+#pragma unroll
+              for (int j = 1; j < NPF; ++j)   // (diagnostic: other rows of Y, in range)
+                pf[k][q][j] = j < npf ? bload(yr, voff, (unsigned)((m0 + trow + j) % M) * ycs4)
+                                      : 0.f;
             }
           }
         }
@@ -658,6 +674,8 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
             float val = smem[lr * BN + lane + 64 * q] + bv;
             if (RELU) val = fmaxf(val, 0.f);
             if constexpr (ACCUM) val += pf[k][q][0];
+#pragma unroll
+            for (int j = 1; j < NPF; ++j) val += pf[k][q][j];
             bstore(yr, val, voff, soff);
           }
         }
@@ -1479,7 +1497,8 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   a.B = B;
   fwd_divisors(a);
   hipStream_t st = (hipStream_t)stream;
-  const bool rl = relu != 0, ac = accumulate != 0;
+  const bool rl = relu != 0;
+  bool ac = accumulate != 0;
   a.x_bytes = plane_bytes(x_bstride, x_cstride, x_tstride, B, K, T, V);
   a.y_bytes = plane_bytes(y_bstride, y_cstride, y_tstride, B, M, T, V);
   a.a_bytes = (unsigned)((long long)M * K * 4);
@@ -1490,6 +1509,23 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   // (W^T read m-contiguous, no bias / relu / accumulate) at M >= SGCN_DIAG_X1B_BOUND stores
   // nothing, i.e. the dAs write a fused shift_in backward epilogue would never make
   if (w_mcontig && !bias && !rl && !ac && M >= SGCN_DIAG_X1B_BOUND) a.y_bytes = 0;
+#endif
+#ifdef SGCN_DIAG_F1B_REAL
+  // timing diagnostic only (results wrong): the gcn input-gradient contraction (see
+  // SGCN_DIAG_F1B_BOUND) as an accumulating launch whose epilogue reads four tensors'
+  // worth per element (the finish pass's x0 / residual-gradient / mask / BatchNorm-input
+  // reads moved into the epilogue) while gcn_dx_finish does nothing: the realistic cost of
+  // fusing that pass into this contraction (the bound alone drops the work)
+  if (!w_mcontig && !bias && !rl && !ac && M > kSmallM) {
+    a.diag_f1b = 1;
+    ac = true;
+  }
+#endif
+#ifdef SGCN_DIAG_F1B_BOUND
+  // timing diagnostic only (results wrong): the Shift_gcn input-gradient contraction
+  // (Linear_weight read k-contiguous as W^T, no bias / relu / accumulate) stores nothing,
+  // and gcn_dx_finish reads no dXt (bn.hip): the whole dXt round trip free
+  if (!w_mcontig && !bias && !rl && !ac) a.y_bytes = 0;
 #endif
 #ifdef SGCN_DIAG_F2_BOUND
   // timing diagnostic only (tools/ab_variant.sh; results are wrong): the stride-2 residual
