@@ -42,9 +42,7 @@ extern "C" {
  * default kernels' argument lists.
  * 23: sgcn_sgd_step flags bit 2 (the (weight_decay, lr) column as the device address of a
  * float pair: hyper-parameters of a graph-captured step read at replay); sgcn_pw_fwd_tshift
- * takes two_row (the two-tap operand of channels with |xpos| < 2^-25); sgcn_pw_fwd_gcn_dx /
- * sgcn_pw_gcn_dx_rows (Shift_gcn's dX contraction with the input-gradient finish in its
- * epilogue). */
+ * takes two_row (the two-tap operand of channels with |xpos| < 2^-25). */
 int sgcn_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
@@ -224,25 +222,6 @@ int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long l
                        void* ws, size_t ws_bytes, float* y, long long y_bstride,
                        long long y_cstride, int relu, int two_row, int B, int M, int K, int T,
                        int V, void* stream);
-
-/* Shift_gcn's input gradient in ONE launch (ABI 23): the dX contraction
- *   dXt[b][c][t][u] = sum_k w[c*K + k] * dz[b][k][t][u]      (w = Linear_weight, (M=C_in, K))
- * and, in its epilogue, what sgcn_gcn_dx_finish does with dXt (which is never stored):
- *   dx[b][c][t][v'] = dXt[b][c][t][u] * m[u*M + c] (+ add1) (+ add2 * (add2_mask > 0) or
- *   + add2), v' = (u + c) mod V (index_select with shift_in transposed + the feature mask,
- *   shift_gcn.py:125-129); dx is bit-identical to sgcn_pw_fwd + sgcn_gcn_dx_finish.
- * The two reductions come out per position tile instead of per plane:
- *   dmask_part[tile][c][u] = sum over the tile of dXt[.][c][.][u] * x0[.][c][.][v'];
- *   prev_part[tile][c] (float2, optional) = {sum g, sum g * (prev_s - prev_mean[c]) *
- *   prev_invstd[c]}, g = dx * (x0 > 0) (the previous unit's bn2 backward partials).
- * Feed them to sgcn_mask_grad_finalize / sgcn_bn_bwd_finalize with B = the tile count,
- * sgcn_pw_gcn_dx_rows(B, M, T, V). Requires 4 < M <= 256, V <= 64. */
-int sgcn_pw_gcn_dx_rows(int B, int M, int T, int V);
-int sgcn_pw_fwd_gcn_dx(const float* w, const float* dz, const float* x0, const float* m,
-                       const float* add1, const float* add2, const float* add2_mask,
-                       const float* prev_s, const float* prev_mean, const float* prev_invstd,
-                       float* dx, float* dmask_part, float* prev_part, int B, int M, int K,
-                       int T, int V, void* stream);
 
 /* Workspace bytes for sgcn_pw_dw. */
 size_t sgcn_pw_dw_ws_bytes(int B, int M, int Nc, int T, int V);

@@ -91,11 +91,6 @@ struct FwdArgs {
   // extent loads 0 / drops the store) and epilogue flags
   unsigned x_bytes, y_bytes, a_bytes, mask_bytes;
   int relu;
-  // GXF (sgcn_pw_fwd_gcn_dx): Shift_gcn's input-gradient finish in the epilogue; all in the
-  // layout of y except gmask (V x M) and the per-channel gpmean / gpinvstd
-  const float *gx0, *gadd1, *gadd2, *gadd2m, *gps, *gpmean, *gpinvstd, *gmask;
-  float* gdmask;   // [tiles][M][V] mask-gradient partials
-  float* gbnpart;  // [tiles][M] float2: the previous unit's bn2 backward partials
 #ifdef SGCN_DIAG_F1B_REAL
   int diag_f1b;
 #endif
@@ -291,10 +286,9 @@ __global__ __launch_bounds__(256) void tshift_two_row_flag_kernel(int K,
 // the prologue and B is single-buffered (a second barrier per stage): 35 instead of 43 KB of
 // LDS, so four workgroups fit a CU instead of three — a third more operand bytes in flight.
 template <int BM, int BN, int WM, int WN, bool MASK, bool XROT, bool AMC, bool ACCUM,
-          bool TSH = false, bool AR = false, bool GXF = false>
+          bool TSH = false, bool AR = false>
 __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   SGCN_CRIT_PRIO();
-  static_assert(!GXF || (!MASK && !XROT && !AMC && !ACCUM && !TSH), "GXF: the gcn dX form");
   static_assert(!TSH || (!MASK && !XROT), "the temporal-shift operand is plain");
   static_assert(!AR || !TSH, "AR: plain contraction");
   constexpr int NT = 64 * WM * WN;
@@ -688,123 +682,7 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         __syncthreads();
       }
   };
-  // GXF (round 6): Shift_gcn's input-gradient finish (what sgcn_gcn_dx_finish does with the
-  // stored dXt, bn.hip) applied to the staged rows: the tile holds dXt[c][(t, u)] for its
-  // channels c and positions; the output dx[c][(t, v')] with v' = (u + c) mod V is the
-  // rotated store (y.rsign = +1), dx = dXt * m[u][c] (+ add1) (+ add2 masked by add2m > 0)
-  // in the finish kernel's order (bit-identical dx), and the two reductions it made per
-  // plane come out per tile: the mask-gradient partial sum_t dXt * x0[v'] per (tile, c, u)
-  // (the row's products through LDS, joint u summed by lane u in column order) and the
-  // previous bn2's backward partials {sum g, sum g * (s - mean) * invstd}, g = dx * (x0 > 0),
-  // per (tile, c) (a wave reduction). dXt is never written or read back.
-  auto epilogue_gxf = [&]() {
-#pragma clang fp contract(off)
-    const unsigned yb = p.y_bytes;
-    const auto x0r = make_rsrc(p.gx0, yb);
-    const auto a1r = make_rsrc(p.gadd1 ? p.gadd1 : p.gx0, p.gadd1 ? yb : 0u);
-    const auto a2r = make_rsrc(p.gadd2 ? p.gadd2 : p.gx0, p.gadd2 ? yb : 0u);
-    const auto amr = make_rsrc(p.gadd2m ? p.gadd2m : p.gx0, p.gadd2m ? yb : 0u);
-    const auto psr = make_rsrc(p.gps ? p.gps : p.gx0, p.gps ? yb : 0u);
-    const auto gmr = make_rsrc(p.gmask, (unsigned)(V * M * 4));
-    const bool has1 = p.gadd1 != nullptr, has2 = p.gadd2 != nullptr;
-    const bool hasm = p.gadd2m != nullptr, part = p.gps != nullptr;
-    const int tile = p0 / BN;
-    // lane u < V sums the columns of joint u: k = j0, j0 + V, ... (joint of column k is
-    // (p0 + k) mod V)
-    const int pv = p0 % V;
-    const int j0 = lane < V ? (lane - pv < 0 ? lane - pv + V : lane - pv) : BN;
-    const auto pmr = make_rsrc(p.gpmean ? p.gpmean : p.gx0, p.gpmean ? (unsigned)(M * 4) : 0u);
-    const auto pir = make_rsrc(p.gpinvstd ? p.gpinvstd : p.gx0, p.gpinvstd ? (unsigned)(M * 4) : 0u);
-    float fx[RPW][CQ], f1[RPW][CQ], f2[RPW][CQ], fm[RPW][CQ], fs[RPW][CQ], mv[RPW][CQ];
-    float pmv[RPW], piv[RPW];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        // every global operand of this wave's rows of the pass, before the LDS staging
-#pragma unroll
-        for (int k = 0; k < RPW; ++k) {
-          const int trow = row_of(i, h, k);
-          const int c = m0 + trow;
-          const unsigned soff = c < M ? (unsigned)c * ycs4 : yb;
-          pmv[k] = bload(pmr, 0u, (unsigned)min(c, M - 1) * 4u);
-          piv[k] = bload(pir, 0u, (unsigned)min(c, M - 1) * 4u);
-#pragma unroll
-          for (int q = 0; q < CQ; ++q) {
-            int vo = vq[q] + rot_s[trow];
-            vo = vo >= V ? vo - V : vo;
-            const unsigned voff = ycolq[q] + (unsigned)(vo * 4);
-            fx[k][q] = bload(x0r, voff, soff);
-            f1[k][q] = bload(a1r, voff, soff);
-            f2[k][q] = bload(a2r, voff, soff);
-            fm[k][q] = bload(amr, voff, soff);
-            fs[k][q] = bload(psr, voff, soff);
-            mv[k][q] = bload(gmr, (unsigned)(vq[q] * M * 4), (unsigned)min(c, M - 1) * 4u);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int rr = 0; rr < 8; ++rr) {
-            const int r = 8 * h + rr;
-            const int lr = wm * 16 + (r & 3) + 8 * ((r >> 2) & 1) + 4 * kl;
-            smem[lr * BN + wn * (BN / WN) + j * 32 + cl] = acc[i][j][r];
-          }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < RPW; ++k) {
-          const int lr = wid + k * NW;
-          const int trow = row_of(i, h, k);
-          const int c = m0 + trow;
-          if (c >= M) break;   // rows past M (they increase with k)
-          const float bv = bias_s[trow];
-          const unsigned soff = (unsigned)c * ycs4;
-          const float pm = pmv[k], pi = piv[k];
-          float b0 = 0.f, b1 = 0.f;
-#pragma unroll
-          for (int q = 0; q < CQ; ++q) {
-            int vo = vq[q] + rot_s[trow];
-            vo = vo >= V ? vo - V : vo;
-            const unsigned voff = ycolq[q] + (unsigned)(vo * 4);
-            const float g = smem[lr * BN + lane + 64 * q] + bv;   // dXt (as stored before)
-            // sgcn_gcn_dx_finish's arithmetic as compiled there: dXt * m + add1 as one fma,
-            // then + add2 (or dXt * m + add2 as one fma without add1)
-            const float a2 = hasm ? (fm[k][q] > 0.f ? f2[k][q] : 0.f) : f2[k][q];
-            float val;
-            if (has1) {
-              val = fmaf(g, mv[k][q], f1[k][q]);
-              if (has2) val = val + a2;
-            } else {
-              val = has2 ? fmaf(g, mv[k][q], a2) : g * mv[k][q];
-            }
-            bstore(yr, val, voff, soff);
-            smem[lr * BN + lane + 64 * q] = g * fx[k][q];   // the mask-gradient product
-            const float gg = fx[k][q] > 0.f ? val : 0.f;       // x0 = 0 past the plane
-            b0 += gg;
-            b1 = fmaf(gg, (fs[k][q] - pm) * pi, b1);
-          }
-          if (part) {
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-              b0 += __shfl_xor(b0, o, 64);
-              b1 += __shfl_xor(b1, o, 64);
-            }
-            if (lane == 0)
-              reinterpret_cast<float2*>(p.gbnpart)[(size_t)tile * M + c] = make_float2(b0, b1);
-          }
-          // (the row's products were written by this wave's own lanes: LDS is in order)
-          if (lane < V) {
-            float sm = 0.f;
-            for (int kk = j0; kk < BN; kk += V) sm += smem[lr * BN + kk];
-            p.gdmask[((size_t)tile * M + c) * V + lane] = sm;
-          }
-        }
-        __syncthreads();
-      }
-  };
-  if constexpr (GXF) {
-    epilogue_gxf();
-  } else if (rotated) {
+  if (rotated) {
     if (p.relu) epilogue(std::true_type{}, std::true_type{});
     else epilogue(std::false_type{}, std::true_type{});
   } else {
@@ -1434,14 +1312,6 @@ __global__ __launch_bounds__(256) void pw_fwd_smallm_kernel(FwdArgs p) {
 // launch helpers
 // ------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool AR = false>
-void launch_pwg_gxf(const FwdArgs& a, hipStream_t st) {
-  const long long P = (long long)a.B * a.T * a.V;
-  dim3 grid((unsigned)((P + BN - 1) / BN), (a.M + BM - 1) / BM);
-  pwg_fwd_kernel<BM, BN, WM, WN, false, false, false, false, false, AR, true>
-      <<<grid, 64 * WM * WN, 0, st>>>(a);
-}
-
-template <int BM, int BN, int WM, int WN, bool AR = false>
 void launch_pwg(const FwdArgs& a, bool accum, hipStream_t st) {
   const long long P = (long long)a.B * a.T * a.V;   // < 2^31 (checked by the caller)
   dim3 grid((unsigned)((P + BN - 1) / BN), (a.M + BM - 1) / BM);
@@ -1684,70 +1554,6 @@ int sgcn_pw_fwd(const float* w, int w_mcontig, const float* bias, const float* x
   // tiles at M > 128 measured there too, not better)
   else if (M <= 128) launch_pwg<128, 128, 4, 2>(a, ac, st);
   else launch_pwg<256, 128, 4, 2>(a, ac, st);
-  SGCN_LAUNCH_CHECK();
-  return 0;
-}
-
-// the position-tile width of the gcn input-gradient contraction at M rows (its partial rows)
-static int gcn_dx_bn(int M) { return M <= 64 ? 256 : 128; }
-
-int sgcn_pw_gcn_dx_rows(int B, int M, int T, int V) {
-  const long long P = (long long)B * T * V;
-  return (int)((P + gcn_dx_bn(M) - 1) / gcn_dx_bn(M));
-}
-
-int sgcn_pw_fwd_gcn_dx(const float* w, const float* dz, const float* x0, const float* m,
-                       const float* add1, const float* add2, const float* add2_mask,
-                       const float* prev_s, const float* prev_mean, const float* prev_invstd,
-                       float* dx, float* dmask_part, float* prev_part, int B, int M, int K,
-                       int T, int V, void* stream) {
-  SGCN_REQUIRE(B >= 0 && M > kSmallM && M <= 256 && K > 0 && K <= 256 && T >= 0 && V > 0 &&
-               V <= 64);
-  SGCN_REQUIRE((long long)B * T * V < (1LL << 31));
-  SGCN_REQUIRE((long long)B * (M > K ? M : K) * T * V < (1LL << 29));
-  SGCN_REQUIRE(!prev_part || (prev_s && prev_mean && prev_invstd));
-  SGCN_REQUIRE(!add2_mask || add2);
-  if (B == 0 || T == 0) return 0;
-  SGCN_REQUIRE(w && dz && x0 && m && dx && dmask_part);
-  const long long N = (long long)T * V;
-  FwdArgs a{};
-  a.A = w;                      // Linear_weight (M = C_in, K = C_out): A[m][k] = w[m*K + k]
-  a.lda = K;
-  a.a_mcontig = 0;
-  a.bias = nullptr;
-  a.x = {dz, (long long)K * N, N, 1, 0};
-  a.mask = nullptr;
-  a.y = {dx, (long long)M * N, N, 1, 1};   // stored at v' = (u + c) mod V
-  a.M = M;
-  a.K = K;
-  a.T = T;
-  a.V = V;
-  a.B = B;
-  fwd_divisors(a);
-  a.x_bytes = plane_bytes(a.x.bstride, a.x.cstride, 1, B, K, T, V);
-  a.y_bytes = plane_bytes(a.y.bstride, a.y.cstride, 1, B, M, T, V);
-  a.a_bytes = (unsigned)((long long)M * K * 4);
-  a.relu = 0;
-  a.gx0 = x0;
-  a.gadd1 = add1;
-  a.gadd2 = add2;
-  a.gadd2m = add2_mask;
-  a.gps = prev_part ? prev_s : nullptr;
-  a.gpmean = prev_part ? prev_mean : nullptr;
-  a.gpinvstd = prev_part ? prev_invstd : nullptr;
-  a.gmask = m;
-  a.gdmask = dmask_part;
-  a.gbnpart = prev_part;
-  hipStream_t st = (hipStream_t)stream;
-  // the tile shapes of sgcn_pw_fwd (gcn_dx_bn gives their position widths)
-  if (M <= 64) {
-    if (K > 16 && K <= 64 && SGCN_PW_AR) launch_pwg_gxf<64, 256, 2, 4, true>(a, st);
-    else launch_pwg_gxf<64, 256, 2, 4>(a, st);
-  } else if (M <= 128) {
-    launch_pwg_gxf<128, 128, 4, 2>(a, st);
-  } else {
-    launch_pwg_gxf<256, 128, 4, 2>(a, st);
-  }
   SGCN_LAUNCH_CHECK();
   return 0;
 }

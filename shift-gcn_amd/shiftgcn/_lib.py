@@ -53,9 +53,6 @@ SIGNATURES = {
     "sgcn_pw_tshift_ws_bytes": (_Z, [_I]),
     "sgcn_pw_fwd_tshift": (_I, [_P, _P, _P, _L, _L, _P, _P, _P, _P, _P, _P, _Z, _P, _L, _L, _I,
                                 _I, _I, _I, _I, _I, _I, _P]),
-    "sgcn_pw_gcn_dx_rows": (_I, [_I, _I, _I, _I]),
-    "sgcn_pw_fwd_gcn_dx": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,
-                                _I, _I, _P]),
     "sgcn_pw_dw_ws_bytes": (_Z, [_I, _I, _I, _I, _I]),
     "sgcn_pw_dw": (_I, [_P, _L, _L, _I, _I, _P, _L, _L, _I, _I, _P, _P, _I, _I, _P, _I, _P, _Z,
                         _I, _I, _I, _I, _I, _P]),

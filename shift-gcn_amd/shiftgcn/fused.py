@@ -358,40 +358,29 @@ def gcn_backward(mod, s: GcnSaved, dH, extra_dx=None, dy_coef=None, prev=None, e
     # a plain plane: G(b,d,n) = dZ[b,d,n]
     dLW = ops.grad_like(mod.Linear_weight)
     dLb = ops.grad_like(mod.Linear_bias)
-    a2, a2m = extra_dx if isinstance(extra_dx, tuple) else (extra_dx, None)
-    if GCN_DX_FUSED and Cin > 4 and V <= 64:
-        # the dX contraction with the input-gradient finish in its epilogue (dXt never
-        # stored); the mask-gradient and previous-bn2 partials come per position tile
-        res = ops.gcn_dx_fused(mod.Linear_weight, dZ, x0, s.m, add1=g_id, add2=a2, prev=prev,
-                               add2_mask=a2m)
-        dx, mpart, mrows = res[:3]
-        if prev is not None:   # the previous unit's bn2 backward partials (x0 = its out)
-            extra_out["prev_part"] = (res[3], mrows)
-    else:
-        dXt = _empty(B, Cin, T, V, like=x0)
-        ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
+    dXt = _empty(B, Cin, T, V, like=x0)
     # on the side stream the weight gradient is enqueued after the dX contraction (it then
     # overlaps the streaming passes that follow instead of competing for the MFMA pipes)
+    ops.pw_fwd(mod.Linear_weight, False, None, PV(dZ), PV(dXt), Cin, Cout, T, V)
     with _OffPath(off, dZ, s.xg):
         ops.pw_dw(PV(dZ), PV(s.xg), dLW, Cout, Cin, T, V, transpose=True, dbias=dLb)
     g["Linear_weight"], g["Linear_bias"] = _late(dLW, off), _late(dLb, off)
-    if not (GCN_DX_FUSED and Cin > 4 and V <= 64):
-        mrows = B
-        if prev is not None:   # also the previous unit's bn2 backward partials
-            dx, mpart, pp = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, prev=prev,
-                                              add2_mask=a2m)
-            extra_out["prev_part"] = (pp, B)
-        else:
-            dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
+    a2, a2m = extra_dx if isinstance(extra_dx, tuple) else (extra_dx, None)
+    if prev is not None:   # also the previous unit's bn2 backward partials (x0 = its out)
+        dx, mpart, extra_out["prev_part"] = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id,
+                                                              add2=a2, prev=prev,
+                                                              add2_mask=a2m)
+    else:
+        dx, mpart = ops.gcn_dx_finish(dXt, x0, s.m, add1=g_id, add2=a2, add2_mask=a2m)
     dmask = ops.grad_like(mod.Feature_Mask)
     fm = mod.Feature_Mask
     if BATCH_SIDE and (off or _defer_ok((fm,))):
         # with the backward's other optimizer-only finalizes (end of the backward)
-        _task(mpart.device).mask.append((mpart, fm, mrows, Cin, V, dmask))
+        _task(mpart.device).mask.append((mpart, fm, B, Cin, V, dmask))
         g["Feature_Mask"] = _Later(dmask)
     else:
         with _OffPath(off, mpart):
-            ops.mask_grad_finalize(mpart, fm, mrows, Cin, V, out=dmask)
+            ops.mask_grad_finalize(mpart, fm, B, Cin, V, out=dmask)
         g["Feature_Mask"] = _late(dmask, off)
     if mod.has_down:
         dWd = ops.grad_like(conv.weight)
@@ -734,17 +723,15 @@ def _unit_backward(unit, s: UnitSaved, dout, off):
     kind = unit.residual_kind
     g = {}
     cached = unit.__dict__.pop("_bwd_part", None)
-    prow = B
     if cached is not None and cached[0] is dout and kind != "conv":
-        # made by the next unit's gcn_dx_finish (per plane) or fused dX launch (per tile)
-        (part, prow), rpart = cached[1], None
+        part, rpart = cached[1], None   # made by the next unit's gcn_dx_finish
     elif kind == "conv":
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False, r=s.rs.Rc,
                                         rst=s.rs.rst)
     else:
         part, rpart = ops.bn_bwd_reduce(dout, s.out, True, S, ts.sst, False)
     coef2, g["tcn1.bn2.weight"], g["tcn1.bn2.bias"] = ops.bn_bwd_finalize(
-        part, prow, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
+        part, B, Cout, B * To * V, ts.sst, unit.tcn1.bn2)
     if kind != "conv" and so.stride == 1 and ops.ra_fits(To * V, V):
         # neither dS nor the identity-residual gradient is written: the shift_out backward
         # forms dS while staging, gcn_dx_finish forms dout*(out > 0)
@@ -812,11 +799,6 @@ TSHIFT_TWO_ROW = int(os.environ.get("SGCN_TSHIFT_TWO_ROW", "2"))
 # after residual.conv) folded into that conv's weights and bias (folded_conv_bn), so the
 # consumer adds the residual without an affine. A/B knob (round 4).
 EVAL_FOLD = int(os.environ.get("SGCN_EVAL_FOLD", "1"))
-# Shift_gcn's input-gradient finish (inverse shift_in rotation x mask, residual-gradient adds,
-# mask-gradient and previous-bn2 partials) in the epilogue of its dX contraction
-# (sgcn_pw_fwd_gcn_dx; round 6): dXt is never stored or read back. Measured -7.6 % NTU /
-# -6.8 % MP same-box (profiles/r06_f1/): off. 1 = fused (A/B knob).
-GCN_DX_FUSED = int(os.environ.get("SGCN_GCN_DX_FUSED", "0"))
 # Shift_gcn.bn's backward sums made by the Shift_tcn.shift_in backward launch
 # (sgcn_tshift_bwd_gbn) instead of a separate sgcn_bn_bwd_reduce pass: 2 = every unit (with a
 # down conv, the down BatchNorm's sums too; round 3), 1 = units without a down conv only

@@ -917,56 +917,6 @@ def gcn_dx_finish(dxt, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
     return (dx, part) if prev is None else (dx, part, pp)
 
 
-def gcn_dx_fused(w, dz, x0, m, add1=None, add2=None, prev=None, add2_mask=None):
-    """Shift_gcn's input gradient in one launch (sgcn_pw_fwd_gcn_dx): the dX contraction
-    with ``w`` = Linear_weight (C_in, C_out) over ``dz`` (B, C_out, T, V), whose epilogue does
-    what :func:`gcn_dx_finish` does with the dXt it never stores. Returns (dx, dmask
-    partials, rows[, prev_part]) — the partials per position tile (``rows`` of them), for
-    mask_grad_finalize / bn_bwd_finalize with B = rows."""
-    B, K, T, V = dz.shape
-    M = w.shape[0]
-    if x0.shape != (B, M, T, V):
-        raise ValueError("x0 must be (B, C_in, T, V)")
-    for t, n in ((w, "weight"), (dz, "grad_output"), (x0, "x0"), (m, "mask")):
-        check_input(t, n)
-    for t, n in ((add1, "add1"), (add2, "add2"), (add2_mask, "add2_mask")):
-        _opt(t, n)
-    lib = _lib.load()
-    # batches past 2^29-element operands run in chunks over B (as pw_fwd); the per-tile
-    # partials of the chunks are consecutive rows
-    plane = max(M, K) * T * V
-    if plane >= PW_MAX_ELEMS:
-        raise ValueError("pointwise operand plane too large for one sample")
-    bc = max(1, min(B, (PW_MAX_ELEMS - 1) // plane))
-    chunks = [(b0, min(bc, B - b0)) for b0 in range(0, B, bc)]
-    crow = [lib.sgcn_pw_gcn_dx_rows(nb, M, T, V) for _, nb in chunks]
-    rows = sum(crow)
-    dev = dz.device
-    dx = torch.empty((B, M, T, V), device=dev, dtype=_F32)
-    part = torch.empty((rows * M * V,), device=dev, dtype=_F32)
-    pp = torch.empty((rows * M * 2,), device=dev, dtype=_F32) if prev is not None else None
-    ps, pst = prev if prev is not None else (None, None)
-    P = B * T * V
-    nb_ = 4 * P * (K + 2 * M + M * sum(t is not None for t in (add1, add2, add2_mask, ps)))
-    sz, sx = K * T * V, M * T * V
-
-    def at(t, b0, per):
-        return None if t is None else t.data_ptr() + 4 * b0 * per
-    with _timed("gcn_dx_fused", 2.0 * P * M * K, nb_, dz, f"M{M} K{K} T{T} V{V}"):
-        r0 = 0
-        for (b0, nb), nr in zip(chunks, crow):
-            rc = lib.sgcn_pw_fwd_gcn_dx(
-                _ptr(w), at(dz, b0, sz), at(x0, b0, sx), _ptr(m), at(add1, b0, sx),
-                at(add2, b0, sx), at(add2_mask, b0, sx), at(ps, b0, sx),
-                _ptr(pst.mean) if pst else None, _ptr(pst.invstd) if pst else None,
-                at(dx, b0, sx), part.data_ptr() + 4 * r0 * M * V,
-                None if pp is None else pp.data_ptr() + 4 * r0 * M * 2, nb, M, K, T, V,
-                _stream(dz))
-            _lib.check(rc, "sgcn_pw_fwd_gcn_dx")
-            r0 += nr
-    return (dx, part, rows) if prev is None else (dx, part, rows, pp)
-
-
 def mask_grad_finalize(part, mask, B, C, V, out=None):
     dmask = torch.empty_like(mask) if out is None else out
     with _timed("finalize", 0, 4 * part.numel(), mask):
