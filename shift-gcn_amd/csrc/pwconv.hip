@@ -24,7 +24,6 @@
 //      deterministic fp32 partial slabs [split][M][N] + row sums (bias grad), reduced in
 //      fixed order by slab_reduce_kernel (optionally transposed, for Linear_weight's
 //      (C_in, C_out) layout).
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -1602,14 +1601,9 @@ int sgcn_pw_fwd_tshift(const float* w, const float* bias, const float* x, long l
   a.a_bytes = (unsigned)((long long)M * K * 4);
   a.mask_bytes = 0u;
   a.relu = relu ? 1 : 0;
-  // (A/B knob while measuring the round-6 two-row operand: SGCN_TSH_TILE=1 takes the
-  // plain path's 128 x 128 tile at 64 < M <= 128)
-  static const int tile_knob = [] {
-    const char* e = getenv("SGCN_TSH_TILE");
-    return e ? atoi(e) : 0;
-  }();
+  // (the plain path's 128 x 128 tile at 64 < M <= 128 measured no better for this operand,
+  // profiles/r06_x1/tshbench_tile128x128.txt)
   if (M <= 64) launch_pwg_tsh<64, 256, 2, 4>(a, st);
-  else if (M <= 128 && tile_knob == 1) launch_pwg_tsh<128, 128, 4, 2>(a, st);
   else if (M <= 128) launch_pwg_tsh<128, 256, 2, 4>(a, st);
   else launch_pwg_tsh<256, 128, 4, 2>(a, st);
   SGCN_LAUNCH_CHECK();
