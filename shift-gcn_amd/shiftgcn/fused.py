@@ -141,6 +141,9 @@ class _Task:
         self.pos, self.mask, self.grads, self.side = [], [], [], False
 
 
+# (device, graph task id) -> _Task. A backward that raises never runs its callback, so its
+# entry (and the tensors it holds) stays; it is not purged by id, because concurrent
+# backwards from other threads share the device's worker thread and a later id may be live.
 _TASKS = {}
 
 
