@@ -1692,7 +1692,13 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
     if (bm == 128 && bn == 128) SGCN_DW(128, 128);
     else if (bm == 128) SGCN_DW(128, 64);
     else if (bn == 128) SGCN_DW(64, 128);
+#ifdef SGCN_DIAG_DW64_SKIP
+    // timing bound only: the 64 x 64 weight gradients are not computed (the slabs keep
+    // whatever they held), the most a dX + dW fusion at C = 64 could remove
+    else if (!plain) SGCN_DW(64, 64);
+#else
     else SGCN_DW(64, 64);
+#endif
 #undef SGCN_DW
   }
   SGCN_LAUNCH_CHECK();
