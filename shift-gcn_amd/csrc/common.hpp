@@ -9,8 +9,7 @@
 // these macros marks the library, and sgcn_abi_version() then carries SGCN_ABI_DIAG_FLAG.
 #if defined(SGCN_PW_DIAG) || defined(SGCN_PW_STAMPS) || defined(SGCN_DIAG_X1B_BOUND) || \
     defined(SGCN_DIAG_F2_BOUND) || defined(SGCN_DIAG_F1B_BOUND) || \
-    defined(SGCN_DIAG_F1B_REAL) || defined(SGCN_DIAG_DW64_SKIP) || \
-    defined(SGCN_DIAG_DUAL_PROXY)
+    defined(SGCN_DIAG_F1B_REAL) || defined(SGCN_DIAG_DW64_SKIP)
 #define SGCN_DIAG_BUILD 1
 #else
 #define SGCN_DIAG_BUILD 0

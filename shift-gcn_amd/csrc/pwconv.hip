@@ -311,14 +311,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   __shared__ int rot_s[BM];
   __shared__ unsigned ycol_s[BN];   // per tile column: byte offset of (b, t) in Y
   __shared__ int v_s[BN];           // per tile column: joint v
-#ifdef SGCN_DIAG_DUAL_PROXY
-  // timing diagnostic only (results wrong): the cost of a dual dX + dW contraction on the
-  // K = M = 64 input-gradient tiles -- one more operand plane read per stage (Y itself, the
-  // same bytes as the weight gradient's X) and as many more MFMAs, into a second accumulator
-  constexpr bool DUAL = AR && AMC && BM == 64;
-  __shared__ float xs2[DUAL ? BK * BP : 1];
-  float r2[DUAL ? B_PER : 1];
-#endif
 
   SGCN_PW_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -347,7 +339,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   int vv = 0, tt = 0;
   unsigned xcol = p.x_bytes;   // out of range: loads return 0
   const bool colok = p0 + nb < P;
-  unsigned ycol2 = p.y_bytes;
   {
     const int pc = p0 + nb;
     unsigned ycol = p.y_bytes;   // out of range: stores dropped
@@ -366,7 +357,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
       ycol_s[nb] = ycol;
       v_s[nb] = vv;
     }
-    ycol2 = pc < P ? ycol + (unsigned)(vv * 4) : p.y_bytes;
   }
   const unsigned xcs4 = (unsigned)(p.x.cstride * 4);
   const int bstep = XROT ? rot_step(KSTEP_B, p.x.rsign, V) : 0;
@@ -445,16 +435,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
         cv = cv >= V ? cv - V : cv;
       }
     }
-#ifdef SGCN_DIAG_DUAL_PROXY
-    if constexpr (DUAL) {
-      const auto yr2 = make_rsrc(p.y.ptr, p.y_bytes);
-#pragma unroll
-      for (int i = 0; i < B_PER; ++i) {
-        const int row = min(k0 + kb0 + i * KSTEP_B, K - 1);
-        r2[i] = bload(yr2, ycol2, (unsigned)row * (unsigned)(p.y.cstride * 4));
-      }
-    }
-#endif
     if (AR) return;   // A is resident (staged in the prologue)
     const unsigned ak0 = AMC ? (unsigned)(k0 * lda * 4) : (unsigned)(k0 * 4);
 #pragma unroll
@@ -507,12 +487,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
       const float val = MASK ? rb[i] * rm[i] : rb[i];
       Bs[AR ? 0 : buf][(kb0 + i * KSTEP_B) * BP + nb] = val;
     }
-#ifdef SGCN_DIAG_DUAL_PROXY
-    if constexpr (DUAL) {
-#pragma unroll
-      for (int i = 0; i < B_PER; ++i) xs2[(kb0 + i * KSTEP_B) * BP + nb] = r2[i];
-    }
-#endif
     if (AR) return;
 #pragma unroll
     for (int i = 0; i < ((SGCN_PW_DIAG & 1) && k0 ? 0 : A_PER); ++i) {
@@ -527,13 +501,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
-#ifdef SGCN_DIAG_DUAL_PROXY
-  f32x16 acc2[DUAL ? MI : 1][DUAL ? NJ : 1];
-#pragma unroll
-  for (int i = 0; i < (DUAL ? MI : 1); ++i)
-#pragma unroll
-    for (int j = 0; j < (DUAL ? NJ : 1); ++j) acc2[i][j] = f32x16{};
-#endif
 
   const int kl = lane >> 5, cl = lane & 31;
   const int nstage = (K + BK - 1) / BK;
@@ -599,24 +566,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[c2][i], bf[c2][j], acc[i][j],
                                                            0, 0, 0);
     }
-#ifdef SGCN_DIAG_DUAL_PROXY
-    if constexpr (DUAL) {
-      const float* __restrict__ X2 = xs2 + kl * BP + wm * 32 + cl;
-#pragma unroll
-      for (int kk = 0; kk < BK; kk += 2) {
-        float a2[MI], b2[NJ];
-#pragma unroll
-        for (int i = 0; i < MI; ++i) a2[i] = X2[kk * BP + i * 32];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) b2[j] = Bw[kk * BP + j * 32];
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[i], b2[j], acc2[i][j], 0, 0, 0);
-      }
-    }
-#endif
     if (s + 1 < nstage) {
       if (AR) __syncthreads();   // single B buffer: every wave has read this stage
       store_stage(cur ^ 1, (s + 1) * BK);
@@ -625,18 +574,6 @@ __global__ __launch_bounds__(64 * WM * WN) void pwg_fwd_kernel(FwdArgs p) {
   }
 
   SGCN_PW_STAMP(2);
-#ifdef SGCN_DIAG_DUAL_PROXY
-  if constexpr (DUAL) {
-    float sink = 0.f;
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sink += acc2[i][j][r];
-    if (p.divN_m == 0xFFFFFFFFu) p.y.ptr[tid] = sink;   // never true: keeps acc2 computed
-  }
-#endif
   // ---- epilogue. The MFMA C/D map (col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5))
   // leaves each wave holding 32-column pieces of 64 rows; stored straight from registers,
   // a 128-B line of a Y row is completed by several waves (and tiles) at different times,
@@ -1755,7 +1692,7 @@ int sgcn_pw_dw(const float* g, long long g_bstride, long long g_cstride, int g_t
     if (bm == 128 && bn == 128) SGCN_DW(128, 128);
     else if (bm == 128) SGCN_DW(128, 64);
     else if (bn == 128) SGCN_DW(64, 128);
-#if defined(SGCN_DIAG_DW64_SKIP) || defined(SGCN_DIAG_DUAL_PROXY)
+#ifdef SGCN_DIAG_DW64_SKIP
     // timing bound only: the 64 x 64 weight gradients are not computed (the slabs keep
     // whatever they held), the most a dX + dW fusion at C = 64 could remove
     else if (!plain) SGCN_DW(64, 64);

@@ -56,7 +56,7 @@ def test_cpu_tensor_raises_like_reference():
 
 DIAG_MACROS = ["-DSGCN_PW_DIAG=1", "-DSGCN_PW_STAMPS", "-DSGCN_DIAG_X1B_BOUND=128",
                "-DSGCN_DIAG_F2_BOUND", "-DSGCN_DIAG_F1B_BOUND", "-DSGCN_DIAG_F1B_REAL",
-               "-DSGCN_DIAG_DW64_SKIP", "-DSGCN_DIAG_DUAL_PROXY"]
+               "-DSGCN_DIAG_DW64_SKIP"]
 
 
 @pytest.mark.parametrize("flag", DIAG_MACROS)
